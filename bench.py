@@ -1,0 +1,206 @@
+"""bench.py — Mray/s + ms/frame of the MI355X path-tracing compute path (BASELINE.json metric).
+
+Default workload (N=1): BASELINE.json configs[1] = Cornell box (34 triangles + 4 spheres), 1920x1080, 1 spp,
+maxBounceCount 4, progressive frames (renderedFramesCount = 0, 1, 2, ...). A "step" is one frame: one
+wcpt_render over the whole frame (with N ranks: each rank renders its row block, SURVEY.md §8(e), and the
+blocks are gathered to rank 0 over RCCL). Rays = ray segments = Intersect() calls, counted exactly by the
+instrumented kernel for the very frames that were timed (untimed re-run).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4] [--no-cpu-baseline]
+
+Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+# torch first: libwcpt.so then binds to the HIP runtime torch already loaded (one runtime per process).
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "wc-path-tracer_amd")]
+
+import numpy as np  # noqa: E402
+import wcpt  # noqa: E402
+from wcpt import scene as wscene  # noqa: E402
+from wcpt.dist import row_block  # noqa: E402
+
+CONFIGS = {
+    # name: (scene, width, height, spp, maxBounceCount, description)
+    "c1": ("cornell", 256, 256, 1, 1, "Cornell box (34 tris), 256x256, 1 spp, 1 bounce"),
+    "c2": ("cornell", 1920, 1080, 1, 4, "Cornell box (34 tris), 1920x1080, 1 spp, 4 bounces"),
+    "c3": ("atrium", 1920, 1080, 1, 4, "Sponza-scale atrium OBJ (262k tris), 1920x1080, 1 spp, 4 bounces"),
+    "c4": ("atrium", 3840, 2160, 16, 4, "Sponza-scale atrium OBJ (262k tris), 3840x2160, 16 spp, 4 bounces"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def algorithmic_bytes(c: dict) -> int:
+    """B_seg = 20*S + sum_draw[32*N_pop + 64*N_interior + 48*N_tri] + 60*[hit] + 28*N_draw,
+    plus 164 (SceneData) + 32 (image read-modify-write) per pixel."""
+    return (20 * c["sphere_tests"] + 32 * c["node_pops"] + 64 * c["interior_visits"] + 48 * c["triangle_tests"]
+            + 60 * c["hits"] + 28 * c["draw_fetches"] + (164 + 32) * c["pixels"])
+
+
+def cpu_baseline(scene, width, height, spp, bounces, budget_s=12.0):
+    """The CPU oracle (a scalar C restatement of pathTracer.comp, oracle/pt_oracle.c) on host cores, over a
+    bounded sample of the same frame: bands of rows spread over the image, until ~budget_s of CPU time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure, used here only as the reported CPU baseline
+    threads = max(1, min(16, os.cpu_count() or 1))
+    band = max(threads, 16)
+    sd = scene.scene_data(width, height, max_bounce=bounces, samples=spp, frame=0)
+    meshes = [(m.positions, m.indices, m.nodes) for m in scene.meshes]
+    starts = list(range(0, height - band + 1, max(band, height // 16)))
+    order = starts[0::2] + starts[1::2]
+    t_total, seg, px, done = 0.0, 0, 0, []
+    for y0 in order:
+        t0 = time.perf_counter()
+        _, c = oracle.render(sd, scene.materials, scene.spheres, meshes, width, height, y0=y0, rows=band,
+                             threads=threads)
+        t_total += time.perf_counter() - t0
+        seg += c["segments"]
+        px += c["pixels"]
+        done.append(y0)
+        if t_total >= budget_s:
+            break
+    return {"value": round(seg / t_total / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"{len(done)} bands of {band} rows ({px} px, {seg} segments) of the same frame, frame 0, "
+                      f"{t_total:.1f} s on {threads} threads; CPU oracle oracle/pt_oracle.c (lavapipe absent)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--kernel", type=int, default=wcpt.KERNEL_MEGAKERNEL)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    name, W, H, spp, bounces, desc = CONFIGS[args.config]
+    scene = wscene.generate(name)
+    y0, rows = row_block(H, world, rank)
+    stream = torch.cuda.current_stream()
+
+    ctx = wcpt.Context(local)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.set_kernel(args.kernel)
+    dev = wcpt.DeviceScene(ctx, scene)
+    ctx.create_screen(W, H)
+    ctx.set_row_range(y0, rows)
+    max_rows = -(-H // world)
+    shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
+    ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
+    gathered = [torch.empty_like(shard) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step(frame):
+        sd = scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=frame)
+        ctx.render(sd, *dev.addresses())
+        if world > 1:
+            dist.gather(shard, gathered, dst=0)
+
+    for f in range(args.warmup):
+        step(f)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.profile_begin()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = ctx.profile_end()
+    ctx.sync()  # surfaces a traversal-stack overflow, if any
+
+    # exact work of the timed frames (instrumented kernel, untimed)
+    tot = {k: 0 for k in wcpt.COUNTER_FIELDS}
+    for k in range(args.steps):
+        sd = scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=args.warmup + k)
+        c = ctx.render_counters(sd, *dev.addresses())
+        for n in tot:
+            tot[n] += c[n]
+    t = torch.tensor([elapsed, float(tot["segments"]), float(tot["pixels"] * spp)], dtype=torch.float64,
+                     device="cuda")
+    if world > 1:
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed_max, segs_all, prim_all = float(tmax[0]), float(tsum[0]), float(tsum[1])
+    else:
+        elapsed_max, segs_all, prim_all = elapsed, float(t[1]), float(t[2])
+
+    if rank == 0:
+        ms_per_step = elapsed_max / args.steps * 1e3
+        value = segs_all / elapsed_max / 1e6
+        avg_kernel_s = kernel_ms / max(1, launches) / 1e3
+        bytes_per_launch = algorithmic_bytes(tot) / args.steps
+        achieved = bytes_per_launch / avg_kernel_s / 1e9
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            try:
+                pm = json.load(open(args.pmc_json))
+                if pm.get("config") == args.config and pm.get("kernel") == args.kernel:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "Mray/s (ray segments) + ms/frame at 1920x1080 1spp; achieved HBM GB/s vs peak",
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural scene generated in-process, no dataset)",
+            "config": {"workload": desc, "config": args.config, "scene": name, "width": W, "height": H,
+                       "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
+                       "kernel": ["megakernel", "persistent", "wavefront"][args.kernel],
+                       "parallelism": f"row-block x{world}" + (" + RCCL gather" if world > 1 else "")},
+            "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
+            "segments_per_frame": int(segs_all / args.steps),
+            "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene, W, H, spp, bounces, budget_s=args.cpu_seconds)
+            out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+
+    ctx.set_external_image(0, 0)
+    dev.free()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

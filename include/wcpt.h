@@ -1,0 +1,246 @@
+/*
+ * wcpt.h — C-ABI drop-in boundary for the WC-Path-tracer compute path on MI355X (gfx950).
+ *
+ * This header is the only interface the reference's Jai host would see. It replaces the
+ * Vulkan compute dispatch of `src/PathTracingRenderer.jai` (reference @ /root/reference):
+ *
+ *   reference (file:line)                                   replaced by
+ *   -----------------------------------------------------   -----------------------------------------
+ *   DBufferManager Allocate   src/BufferManager.jai:19-34    wcpt_buffer_alloc
+ *   DBufferManager Update     src/BufferManager.jai:52-64    wcpt_buffer_upload   (grow-on-demand, :53-54)
+ *   DBufferManager Free       src/BufferManager.jai:36-45    wcpt_buffer_free
+ *   GetDeviceAddress          modules/VKUtils/Buffer.jai:101  wcpt_buffer_device_address
+ *   CreateScreen              src/PathTracingRenderer.jai:345 wcpt_create_screen  (rgba32f image -> float4[H][W])
+ *   Resize                    src/PathTracingRenderer.jai:393 wcpt_resize
+ *   Render (push block + vkCmdDispatch)
+ *                             src/PathTracingRenderer.jai:399-457  wcpt_render (SceneData by value + 3 BDAs)
+ *   Submit / timeline wait    modules/VKUtils/Synchronization.jai:64-89, src/main.jai:73-95  wcpt_sync
+ *   Deinit                    src/PathTracingRenderer.jai:473 wcpt_destroy
+ *
+ * Byte layouts of the POD types are the reference's GLSL `scalar` block layouts, which are identical to
+ * the Jai structs (src/shaders/pathTracer.comp:10-95, src/PathTracingRenderer.jai:38-140).
+ *
+ * Errors: every entry point returns int (0 = success, negative = error; -1..-13 keep VkResult meaning).
+ * Nothing aborts or exits. wcpt_last_error() gives a human-readable message.
+ * Threading: one context per device; calls on one context are not thread-safe (the reference drives the
+ * renderer from a single thread, src/main.jai:185-194).
+ */
+#ifndef WCPT_H
+#define WCPT_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WCPT_ABI_VERSION 1
+
+/* ---- error codes (VkResult-compatible where a VkResult exists) ---------------------------------- */
+#define WCPT_SUCCESS                      0
+#define WCPT_ERROR_OUT_OF_HOST_MEMORY    (-1)
+#define WCPT_ERROR_OUT_OF_DEVICE_MEMORY  (-2)
+#define WCPT_ERROR_INITIALIZATION_FAILED (-3)
+#define WCPT_ERROR_DEVICE_LOST           (-4)
+#define WCPT_ERROR_UNKNOWN               (-13)
+#define WCPT_ERROR_INVALID_ARGUMENT      (-1000)
+#define WCPT_ERROR_INVALID_HANDLE        (-1001)
+#define WCPT_ERROR_STACK_OVERFLOW        (-1002) /* BVH deeper than the traversal stack */
+#define WCPT_ERROR_NO_SCREEN             (-1003) /* wcpt_render before wcpt_create_screen */
+#define WCPT_ERROR_PARSE                 (-1004) /* OBJ text could not be parsed */
+
+/* ---- material types (pathTracer.comp:30-33, PathTracingRenderer.jai:53-56) ---------------------- */
+#define WCPT_MATERIAL_METAL      0u
+#define WCPT_MATERIAL_DIELECTRIC 1u
+
+/* ---- kernel variants ---------------------------------------------------------------------------- */
+#define WCPT_KERNEL_MEGAKERNEL  0  /* one lane per pixel, exact reference semantics (default)          */
+#define WCPT_KERNEL_PERSISTENT  1  /* persistent waves, lanes refill with new pixels (same semantics)  */
+#define WCPT_KERNEL_WAVEFRONT   2  /* split ray-gen / traverse / shade queues (same semantics)         */
+
+/* ---- POD types with the reference byte layouts -------------------------------------------------- */
+
+/* SceneData — pathTracer.comp:10-22 == PathTracingRenderer.jai:38-51. 164 bytes.
+ * Matrices are column-major (GLSL mat4), as the Jai host uploads them after transpose()
+ * (PathTracingRenderer.jai:28,33). */
+typedef struct wcpt_scene_data {
+    float    inverseProjection[16]; /*   0 */
+    float    inverseView[16];       /*  64 */
+    float    position[3];           /* 128 */
+    uint32_t maxBounceCount;        /* 140  (Jai default 3) */
+    uint32_t samples;               /* 144  (Jai default 1) */
+    uint32_t sphereCount;           /* 148 */
+    uint32_t drawCommandCount;      /* 152 */
+    uint32_t renderedFramesCount;   /* 156 */
+    uint32_t boxID;                 /* 160  (unused by the kernel) */
+} wcpt_scene_data;
+
+/* Material — pathTracer.comp:35-47 == PathTracingRenderer.jai:58-70. 60 bytes. */
+typedef struct wcpt_material {
+    uint32_t type;                  /*  0  WCPT_MATERIAL_* (Jai default METAL) */
+    float    albedo[3];             /*  4 */
+    float    emission[3];           /* 16 */
+    float    emissionStrength;      /* 28  (Jai default 0) */
+    float    metallic;              /* 32  (unused by the kernel) */
+    float    roughness;             /* 36 */
+    float    absorption[3];         /* 40 */
+    float    absorptionStrength;    /* 52  (Jai default 1) */
+    float    ior;                   /* 56  (Jai default 1) */
+} wcpt_material;
+
+/* Sphere — pathTracer.comp:60-64 == PathTracingRenderer.jai:86-90. 20 bytes. */
+typedef struct wcpt_sphere {
+    float    position[3];
+    float    radius;
+    uint32_t material;
+} wcpt_sphere;
+
+/* Node — pathTracer.comp:66-72 == PathTracingRenderer.jai:125-134. 32 bytes.
+ * triangleCount counts INDICES (3 per triangle); 0 means interior, whose children are at
+ * leftNodeOrTriangleIndex and leftNodeOrTriangleIndex+1. */
+typedef struct wcpt_node {
+    float    min[3];
+    float    max[3];
+    uint32_t leftNodeOrTriangleIndex;
+    uint32_t triangleCount;
+} wcpt_node;
+
+/* DrawCommand — pathTracer.comp:82-87 == PathTracingRenderer.jai:135-140. The array stride is the Jai
+ * size_of = 32 bytes (28 bytes of fields + 4 bytes tail padding). The three fields are device
+ * addresses from wcpt_buffer_device_address(). indexCount is not read by the kernel. */
+typedef struct wcpt_draw_command {
+    uint64_t vertexBuffer;          /* -> float[3] positions, stride 12 */
+    uint64_t indexBuffer;           /* -> uint32 indices (BVH-permuted) */
+    uint64_t bvhBuffer;             /* -> wcpt_node[] */
+    uint32_t indexCount;
+    uint32_t _pad;
+} wcpt_draw_command;
+
+/* Camera — PathTracingRenderer.jai:6-20 (the Jai Matrix4s are stored here already in the column-major
+ * order the shader reads). */
+typedef struct wcpt_camera {
+    float position[3];
+    float direction[3];
+    float yaw;
+    float pitch;
+    float fov;                      /* vertical, degrees (Jai default 90) */
+    float projection[16];
+    float view[16];
+    float inverseProjection[16];
+    float inverseView[16];
+} wcpt_camera;
+
+/* Per-frame work counters of the reference algorithm; exact integers. */
+typedef struct wcpt_counters {
+    uint64_t pixels;          /* pixels rendered                                                   */
+    uint64_t segments;        /* Intersect() calls = ray segments (the "rays" of Mray/s)          */
+    uint64_t sphere_tests;    /* raySphereIntersect calls                                          */
+    uint64_t node_pops;       /* BVH nodes popped from the stack (reference :158-159)              */
+    uint64_t interior_visits; /* interior nodes whose two children were fetched (:183-184)        */
+    uint64_t triangle_tests;  /* rayTriangleIntersect calls (:170)                                 */
+    uint64_t hits;            /* segments that hit (material fetched, :251)                        */
+    uint64_t draw_fetches;    /* DrawCommand fetches (:153)                                        */
+} wcpt_counters;
+
+/* Host mesh produced by the OBJ loader (ModelLoader.jai:60-141) or a scene generator. Memory is owned
+ * by the library; release with wcpt_mesh_free. */
+typedef struct wcpt_mesh {
+    float*    positions;      /* vertex_count * 3 floats */
+    uint32_t  vertex_count;
+    uint32_t* indices;        /* index_count uint32 */
+    uint32_t  index_count;
+} wcpt_mesh;
+
+/* Host scene (geometry + materials + spheres + camera). Owned by the library; wcpt_scene_free. */
+typedef struct wcpt_scene {
+    wcpt_mesh      mesh;
+    wcpt_material* materials;
+    uint32_t       material_count;
+    wcpt_sphere*   spheres;
+    uint32_t       sphere_count;
+    wcpt_camera    camera;
+} wcpt_scene;
+
+typedef struct wcpt_context wcpt_context;
+typedef uint64_t wcpt_buffer;      /* 0 is never a valid handle */
+
+/* ---- library / context ---------------------------------------------------------------------------- */
+int         wcpt_abi_version(void);
+int         wcpt_device_count(int* count);
+int         wcpt_create(int device, wcpt_context** out_ctx);
+int         wcpt_destroy(wcpt_context* ctx);                       /* Deinit, PathTracingRenderer.jai:473 */
+const char* wcpt_last_error(const wcpt_context* ctx);              /* ctx may be NULL: last global error */
+int         wcpt_set_stream(wcpt_context* ctx, void* hip_stream);  /* NULL: the context's own stream     */
+int         wcpt_set_kernel(wcpt_context* ctx, int variant);       /* WCPT_KERNEL_*                       */
+
+/* ---- device buffers (BufferManager.jai) ------------------------------------------------------------ */
+int      wcpt_buffer_alloc(wcpt_context* ctx, uint64_t bytes, wcpt_buffer* out);
+int      wcpt_buffer_upload(wcpt_context* ctx, wcpt_buffer buf, const void* src, uint64_t bytes,
+                            uint64_t offset);  /* grows (reallocates) when offset+bytes > size, like :53-54 */
+int      wcpt_buffer_download(wcpt_context* ctx, wcpt_buffer buf, void* dst, uint64_t bytes,
+                              uint64_t offset);
+int      wcpt_buffer_size(wcpt_context* ctx, wcpt_buffer buf, uint64_t* out_bytes);
+uint64_t wcpt_buffer_device_address(wcpt_context* ctx, wcpt_buffer buf); /* 0 on error */
+int      wcpt_buffer_free(wcpt_context* ctx, wcpt_buffer buf);
+
+/* ---- output image (CreateScreen / Resize) --------------------------------------------------------- */
+int      wcpt_create_screen(wcpt_context* ctx, uint32_t width, uint32_t height);
+int      wcpt_resize(wcpt_context* ctx, uint32_t width, uint32_t height);
+/* Row-block shard: this context renders and stores only rows [y0, y0+rows) of the width x height
+ * frame (global pixel indices and seeds unchanged). rows == 0 resets to the full frame. */
+int      wcpt_set_row_range(wcpt_context* ctx, uint32_t y0, uint32_t rows);
+uint64_t wcpt_image_device_ptr(wcpt_context* ctx);                 /* float4[rows][width], pitch width*16 */
+/* Render into caller-owned device memory (e.g. a torch tensor handed to RCCL, or imported interop memory)
+ * instead of the context's own image. `bytes` must hold width*rows*16. device_ptr == 0 reverts to the
+ * context-owned image. The caller keeps ownership. */
+int      wcpt_set_external_image(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes);
+int      wcpt_readback(wcpt_context* ctx, float* dst, uint64_t bytes);
+int      wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes); /* seed accumulation */
+
+/* ---- dispatch ---------------------------------------------------------------------------------------- */
+/* The push block of pathTracer.comp:90-95 minus `sdp`: SceneData travels by value. Asynchronous on the
+ * context's stream; the caller owns renderedFramesCount sequencing (PathTracingRenderer.jai:423). */
+int      wcpt_render(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials,
+                     uint64_t spheres, uint64_t draw_commands);
+int      wcpt_sync(wcpt_context* ctx);
+/* Same frame through the instrumented kernel: counts the reference algorithm's work.
+ * Does not write the image. Synchronous. */
+int      wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials,
+                              uint64_t spheres, uint64_t draw_commands, wcpt_counters* out);
+
+/* ---- kernel timing (HIP events on the context's stream) -------------------------------------------- */
+int      wcpt_profile_begin(wcpt_context* ctx);
+int      wcpt_profile_end(wcpt_context* ctx, double* kernel_ms_total, uint32_t* launches);
+
+/* ---- host utilities (no GPU needed) ----------------------------------------------------------------- */
+/* OBJ text -> unique (v,vt,vn) vertices + fan-triangulated indices (ModelLoader.jai:60-141). */
+int      wcpt_obj_parse(const char* text, uint64_t length, wcpt_mesh* out);
+int      wcpt_obj_load(const char* path, wcpt_mesh* out);
+void     wcpt_mesh_free(wcpt_mesh* mesh);
+/* Midpoint BVH (PathTracingRenderer.jai:147-217). Permutes `indices` in place. `nodes` must hold
+ * max_nodes entries; 2*index_count/3 is always enough. */
+int      wcpt_bvh_build(const float* positions, uint32_t vertex_count, uint32_t* indices,
+                        uint32_t index_count, wcpt_node* nodes, uint32_t max_nodes, uint32_t* nodes_used);
+/* Camera Update (PathTracingRenderer.jai:22-36): yaw/pitch/fov/position -> matrices. */
+int      wcpt_camera_update(wcpt_camera* cam, float aspect_ratio);
+/* Scene generators: "default" (reference Init scene, PathTracingRenderer.jai:322-339, without a mesh),
+ * "cornell" (Cornell-class box), "atrium" (deterministic Sponza-scale procedural OBJ, ~260k tris). */
+int      wcpt_scene_generate(const char* name, uint32_t seed, wcpt_scene* out);
+void     wcpt_scene_free(wcpt_scene* scene);
+/* Scene as OBJ text (so the atrium goes through the same loader path as ModelLoader.jai). The returned
+ * string is owned by the library: release with wcpt_string_free. */
+int      wcpt_mesh_to_obj(const wcpt_mesh* mesh, char** out_text, uint64_t* out_length);
+void     wcpt_string_free(char* text);
+
+/* ---- self-test entry points (used by the parity tests; GPU) ---------------------------------------- */
+/* Evaluates device functions on n inputs: fn 0 = pcg_hash, 1 = rand stream (4 per input),
+ * 2 = log, 3 = cos, 4 = exp, 5 = sqrt, 6 = divide(in, in2). Inputs/outputs are host arrays of 32-bit words. */
+int      wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const uint32_t* in2,
+                              uint32_t* out, uint32_t n);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* WCPT_H */

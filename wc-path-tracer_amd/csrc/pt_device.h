@@ -1,0 +1,403 @@
+/*
+ * pt_device.h — device-side building blocks of the path tracer (gfx950).
+ *
+ * Semantics follow src/shaders/pathTracer.comp and src/shaders/include/Random.glsl of the reference
+ * exactly (cited per function). Every expression keeps the reference's operand order and is compiled
+ * with -ffp-contract=off, so that the image is bit-identical to oracle/pt_oracle.c on the same inputs.
+ *
+ * Layout-level differences from the reference (results unchanged):
+ *   - SceneData is a kernel argument (scalar loads from the kernarg segment) instead of a BDA buffer.
+ *   - BVH traversal keeps the nearer child in registers and pushes only the farther one, with the box
+ *     entry distance t0 on the stack. A child whose box test fails statically (t0 > t1 || t1 < 0) is never
+ *     pushed; the dynamic cull (t0 > rec.t) is applied when the child would have been popped. This is
+ *     exactly the reference's pop order and cull set (pathTracer.comp:157-200) with one 64-byte sibling
+ *     fetch per interior node instead of 32 (pop) + 64 (children) bytes.
+ */
+#ifndef WCPT_PT_DEVICE_H
+#define WCPT_PT_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/wcpt.h"
+#include "wcpt_libm.h"
+
+namespace wcpt {
+namespace dev {
+
+/* constants.glsl:4-9 */
+constexpr float kBias = 1e-5f;
+constexpr float kInfinity = 3.402823466e+38f;
+constexpr float kPI = 3.14159265358979323846264338327950288f;
+
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ f3 mk3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ f3 rcp3(f3 a) { return mk3(1.0f / a.x, 1.0f / a.y, 1.0f / a.z); }
+/* GLSL dot: (x*x' + y*y') + z*z' */
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* GLSL cross (4.50 spec §8.5) */
+__device__ __forceinline__ f3 cross(f3 a, f3 b)
+{
+    return mk3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ f3 normalize(f3 v) { return v / sqrtf(dot(v, v)); }
+__device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
+__device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)
+{
+    const float d = dot(N, I);
+    const float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return mk3(0.0f, 0.0f, 0.0f);
+    return eta * I - N * (eta * d + sqrtf(k));
+}
+__device__ __forceinline__ float sign1(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+__device__ __forceinline__ f3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+
+/* ---- Random.glsl:10-56 ------------------------------------------------------------------------- */
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t seed)
+{
+    const uint32_t state = seed * 747796405u + 2891336453u;
+    const uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+/* rand_pcg's output word is the PCG permutation of the *current* state (Random.glsl:18-24); rand() then
+ * overwrites the state with that output (Random.glsl:29-30), discarding the LCG step of :21. */
+__device__ __forceinline__ uint32_t pcg_permute(uint32_t state)
+{
+    const uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+__device__ __forceinline__ float rand_f(uint32_t& state)
+{
+    const uint32_t x = pcg_permute(state);
+    state = x;
+    return (float)x * 2.3283064365386963e-10f; /* uintBitsToFloat(0x2f800000u) = 2^-32 */
+}
+
+__device__ __forceinline__ float RandomValueNormalDistribution(uint32_t& seed)
+{
+    const float theta = 2.0f * kPI * rand_f(seed);
+    const float rho = sqrtf(-2.0f * wcpt_logf(rand_f(seed)));
+    return rho * wcpt_cosf(theta);
+}
+__device__ __forceinline__ f3 RandomDirection(uint32_t& seed)
+{
+    const float x = RandomValueNormalDistribution(seed);
+    const float y = RandomValueNormalDistribution(seed);
+    const float z = RandomValueNormalDistribution(seed);
+    return normalize(mk3(x, y, z));
+}
+
+/* ---- pathTracer.comp:24-28, 50-58 ------------------------------------------------------------- */
+struct Ray { f3 origin, direction, invDirection; };
+struct Hit { f3 p, normal; float t; uint32_t material; bool hit, front; };
+
+/* pathTracer.comp:97-108 — slab test; min/max are IEEE minNum/maxNum (v_min_f32 / v_max_f32). */
+__device__ __forceinline__ void rayBox(const Ray& r, float mnx_, float mny_, float mnz_, float mxx_, float mxy_,
+                                       float mxz_, float& t0, float& t1)
+{
+    const float bx = (mnx_ - r.origin.x) * r.invDirection.x;
+    const float by = (mny_ - r.origin.y) * r.invDirection.y;
+    const float bz = (mnz_ - r.origin.z) * r.invDirection.z;
+    const float tx = (mxx_ - r.origin.x) * r.invDirection.x;
+    const float ty = (mxy_ - r.origin.y) * r.invDirection.y;
+    const float tz = (mxz_ - r.origin.z) * r.invDirection.z;
+    const float mnx = fminf(tx, bx), mny = fminf(ty, by), mnz = fminf(tz, bz);
+    const float mxx = fmaxf(tx, bx), mxy = fmaxf(ty, by), mxz = fmaxf(tz, bz);
+    t0 = fmaxf(fmaxf(mnx, mny), fmaxf(mnx, mnz));
+    t1 = fminf(fminf(mxx, mxy), fminf(mxx, mxz));
+}
+
+/* A BVH node (32 B) as two 16-byte loads: {min.xyz, max.x}, {max.yz, left, count}. */
+struct NodeV { float4 a; uint4 b; };
+__device__ __forceinline__ NodeV load_node(const wcpt_node* __restrict__ bvh, uint32_t i)
+{
+    const float4* p = reinterpret_cast<const float4*>(bvh + i);
+    NodeV n;
+    n.a = p[0];
+    n.b = reinterpret_cast<const uint4*>(p)[1];
+    return n;
+}
+__device__ __forceinline__ void node_box(const Ray& r, const NodeV& n, float& t0, float& t1)
+{
+    /* node = {min.xyz, max.x | max.yz, left, count} */
+    rayBox(r, n.a.x, n.a.y, n.a.z, n.a.w, __uint_as_float(n.b.x), __uint_as_float(n.b.y), t0, t1);
+}
+
+/* pathTracer.comp:110-119, near root only (:141) */
+__device__ __forceinline__ float raySphereNear(const Ray& r, f3 position, float radius)
+{
+    const f3 oc = r.origin - position;
+    const float b = dot(oc, r.direction);
+    const float c = dot(oc, oc) - radius * radius;
+    const float t = b * b - c;
+    if (t < 0.0f) return -1.0f;
+    return -b - sqrtf(t);
+}
+
+/* pathTracer.comp:121-133; returns t or -1 */
+__device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c)
+{
+    const f3 edgeAB = b - a;
+    const f3 edgeAC = c - a;
+    const f3 oa = r.origin - a;
+    const f3 crossRDE2 = cross(r.direction, edgeAC);
+    const float inv = 1.0f / dot(edgeAB, crossRDE2);
+    const f3 crossROAE1 = cross(oa, edgeAB);
+    const float u = dot(oa, crossRDE2) * inv;
+    const float v = dot(r.direction, crossROAE1 * inv);
+    const float t = dot(edgeAC, crossROAE1) * inv;
+    return (t > 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f) ? t : -1.0f;
+}
+
+/* Per-lane work counters; reduced per wave and added to global u64 counters. */
+struct Counters {
+    uint32_t pixels, segments, sphere_tests, node_pops, interior_visits, triangle_tests, hits, draw_fetches;
+};
+
+/* Traversal stack in private (scratch) memory; entries = (node index, box entry t0). */
+template <int N>
+struct PrivateStack {
+    uint32_t idx[N];
+    float t0[N];
+};
+
+/* pathTracer.comp:135-211 */
+template <bool COUNT, int STACK>
+__device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
+                                         const wcpt_draw_command* __restrict__ draws, PrivateStack<STACK>& stk,
+                                         Counters& cnt, bool& overflow)
+{
+    Hit rec;
+    rec.t = kInfinity;
+    rec.hit = false;
+    rec.front = false;
+    rec.material = 0;
+    rec.p = mk3(0.0f, 0.0f, 0.0f);
+    rec.normal = mk3(0.0f, 0.0f, 0.0f);
+    if (COUNT) cnt.segments++;
+
+    for (uint32_t i = 0; i < sd.sphereCount; i++) {
+        const wcpt_sphere& s = spheres[i];
+        const f3 sp = mk3(s.position[0], s.position[1], s.position[2]);
+        const float tempRec = raySphereNear(ray, sp, s.radius);
+        if (COUNT) cnt.sphere_tests++;
+        if (tempRec > 0.0f && tempRec < rec.t) {
+            rec.t = tempRec;
+            rec.p = ray.origin + rec.t * ray.direction;
+            rec.normal = (rec.p - sp) / s.radius;
+            rec.hit = true;
+            rec.material = s.material;
+        }
+    }
+
+    for (uint32_t i = 0; i < sd.drawCommandCount; i++) {
+        const wcpt_node* __restrict__ bvh = reinterpret_cast<const wcpt_node*>(draws[i].bvhBuffer);
+        const uint32_t* __restrict__ indices = reinterpret_cast<const uint32_t*>(draws[i].indexBuffer);
+        const float* __restrict__ vertices = reinterpret_cast<const float*>(draws[i].vertexBuffer);
+        if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
+
+        /* root: pushed untested, popped and tested (:155-162) */
+        NodeV cur = load_node(bvh, 0);
+        float c0, c1;
+        node_box(ray, cur, c0, c1);
+        if (c0 > c1 || c1 < 0.0f || c0 > rec.t) continue;
+        uint32_t curLeft = cur.b.z, curCount = cur.b.w;
+        int sp = 0;
+        for (;;) {
+            if (curCount > 0) {
+                /* leaf (:164-178) */
+                for (uint32_t k = 0; k < curCount; k += 3) {
+                    const uint32_t first = k + curLeft;
+                    const uint32_t ia = indices[first + 0];
+                    const uint32_t ib = indices[first + 1];
+                    const uint32_t ic = indices[first + 2];
+                    const f3 a = ld3(vertices + 3ull * ia);
+                    const f3 b = ld3(vertices + 3ull * ib);
+                    const f3 c = ld3(vertices + 3ull * ic);
+                    const float t = rayTriangle(ray, a, b, c);
+                    if (COUNT) cnt.triangle_tests++;
+                    if (t != -1.0f && t < rec.t) {
+                        rec.t = t;
+                        rec.normal = normalize(cross(b - a, c - a));
+                        rec.hit = true;
+                        rec.material = 0; /* :175 */
+                    }
+                }
+            } else {
+                /* interior (:179-199): fetch both children (64 contiguous bytes), test both boxes */
+                const NodeV L = load_node(bvh, curLeft);
+                const NodeV R = load_node(bvh, curLeft + 1);
+                float l0, l1, r0, r1;
+                node_box(ray, L, l0, l1);
+                node_box(ray, R, r0, r1);
+                if (COUNT) { cnt.interior_visits++; cnt.node_pops += 2; }
+                const float leftDist = (l0 > 0.0f) ? l0 : l1;
+                const float rightDist = (r0 > 0.0f) ? r0 : r1;
+                const bool passL = !(l0 > l1 || l1 < 0.0f);
+                const bool passR = !(r0 > r1 || r1 < 0.0f);
+                /* reference order: left popped first iff leftDist < rightDist */
+                const bool leftFirst = leftDist < rightDist;
+                const uint32_t farIdx = leftFirst ? curLeft + 1 : curLeft;
+                const bool passNear = leftFirst ? passL : passR;
+                const bool passFar = leftFirst ? passR : passL;
+                const float nearT0 = leftFirst ? l0 : r0;
+                const float farT0 = leftFirst ? r0 : l0;
+                if (passFar) {
+                    if (sp < STACK) {
+                        stk.idx[sp] = farIdx;
+                        stk.t0[sp] = farT0;
+                        sp++;
+                    } else {
+                        overflow = true;
+                    }
+                }
+                if (passNear && !(nearT0 > rec.t)) {
+                    const NodeV& N = leftFirst ? L : R;
+                    curLeft = N.b.z;
+                    curCount = N.b.w;
+                    continue;
+                }
+            }
+            /* pop (:157-162) */
+            bool found = false;
+            while (sp > 0) {
+                sp--;
+                const uint32_t ni = stk.idx[sp];
+                const float t0 = stk.t0[sp];
+                if (t0 > rec.t) continue;
+                const uint2 lc = reinterpret_cast<const uint2*>(bvh + ni)[3];
+                curLeft = lc.x;
+                curCount = lc.y;
+                found = true;
+                break;
+            }
+            if (!found) break;
+        }
+    }
+
+    if (rec.hit) {
+        rec.p = ray.origin + rec.t * ray.direction;
+        rec.front = dot(ray.direction, rec.normal) < 0.0f;
+        if (!rec.front) rec.normal = rec.normal * -1.0f;
+        if (COUNT) cnt.hits++;
+    }
+    return rec;
+}
+
+/* pathTracer.comp:213-234 */
+__device__ __forceinline__ float CalculateReflectance(f3 inDir, f3 normal, float iorA, float iorB)
+{
+    const float refractRatio = iorA / iorB;
+    const float cosAngleIn = -dot(inDir, normal);
+    const float sinSqr = refractRatio * refractRatio * (1.0f - cosAngleIn * cosAngleIn);
+    if (sinSqr >= 1.0f) return 1.0f;
+    const float cosRefr = sqrtf(1.0f - sinSqr);
+    const float dPerp = iorA * cosAngleIn + iorB * cosRefr;
+    const float dPar = iorB * cosAngleIn + iorA * cosRefr;
+    if (fminf(dPerp, dPar) < 1e-8f) return 1.0f;
+    float rPerp = (iorA * cosAngleIn - iorB * cosRefr) / dPerp;
+    rPerp *= rPerp;
+    float rPar = (iorB * cosAngleIn - iorA * cosRefr) / dPar;
+    rPar *= rPar;
+    return (rPerp + rPar) / 2.0f;
+}
+
+/* pathTracer.comp:236-239 */
+__device__ __forceinline__ f3 ray_color(const Ray& r)
+{
+    const float a = 0.5f * (r.direction.y + 1.0f);
+    const float ia = 1.0f - a;
+    return mk3(0.5f * ia + 1.0f * a, 0.7f * ia + 1.0f * a, 1.0f * ia + 1.0f * a);
+}
+
+/* pathTracer.comp:241-284 */
+template <bool COUNT, int STACK>
+__device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_data& sd,
+                                       const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
+                                       const wcpt_draw_command* __restrict__ draws, PrivateStack<STACK>& stk,
+                                       Counters& cnt, bool& overflow)
+{
+    f3 totalLight = mk3(0.0f, 0.0f, 0.0f);
+    f3 transmittance = mk3(1.0f, 1.0f, 1.0f);
+    for (uint32_t i = 0; i <= sd.maxBounceCount; i++) {
+        const Hit h = intersect<COUNT, STACK>(ray, sd, spheres, draws, stk, cnt, overflow);
+        if (!h.hit) return totalLight + ray_color(ray) * transmittance;
+
+        const wcpt_material& m = mats[h.material];
+        const uint32_t mtype = m.type;
+        const f3 emission = ld3(m.emission);
+        const float emissionStrength = m.emissionStrength;
+        const float roughness = m.roughness;
+        totalLight = totalLight + (emission * emissionStrength) * transmittance;
+
+        if (mtype == WCPT_MATERIAL_METAL) {
+            ray.origin = h.p + h.normal * kBias;
+            const f3 R = reflect(ray.direction, h.normal);
+            const f3 rd = RandomDirection(rng);
+            ray.direction = normalize(R + roughness * rd);
+            ray.invDirection = rcp3(ray.direction);
+            transmittance = transmittance * ld3(m.albedo);
+        } else {
+            const float ior = m.ior;
+            const float etaI = h.front ? 1.0f : ior;
+            const float etaT = h.front ? ior : 1.0f;
+            const float reflectProb = CalculateReflectance(ray.direction, h.normal, etaI, etaT);
+            const f3 R = reflect(ray.direction, h.normal);
+            const f3 T = refract(ray.direction, h.normal, etaI / etaT);
+            bool followReflection = (T.x == 0.0f && T.y == 0.0f && T.z == 0.0f);
+            if (!followReflection) followReflection = (rand_f(rng) <= reflectProb); /* :273 short-circuit */
+            const f3 rd = RandomDirection(rng);
+            ray.direction = normalize((followReflection ? R : T) + roughness * rd);
+            ray.invDirection = rcp3(ray.direction);
+            if (!followReflection && !h.front) {
+                const f3 e = ((ld3(m.absorption) * -1.0f) * m.absorptionStrength) * h.t;
+                transmittance = transmittance * mk3(wcpt_expf(e.x), wcpt_expf(e.y), wcpt_expf(e.z));
+            }
+            ray.origin = h.p + (kBias * h.normal) * sign1(dot(ray.direction, h.normal));
+        }
+    }
+    return totalLight;
+}
+
+/* pathTracer.comp:290-302 — primary ray direction for pixel (x, y) of a W x H frame. */
+__device__ __forceinline__ f3 primary_direction(const wcpt_scene_data& sd, uint32_t x, uint32_t y, uint32_t W, uint32_t H)
+{
+    const float imgW = (float)W, imgH = (float)H;
+    float cx = (float)x / imgW, cy = (float)y / imgH;
+    cx = cx + (1.0f / imgW) * 0.5f;
+    cy = cy + (1.0f / imgH) * 0.5f;
+    cy = 1.0f - cy;
+    cx = cx * 2.0f - 1.0f;
+    cy = cy * 2.0f - 1.0f;
+    const float* P = sd.inverseProjection;
+    float tg[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) tg[r] = P[0 * 4 + r] * cx + P[1 * 4 + r] * cy + P[2 * 4 + r] * 1.0f + P[3 * 4 + r] * 1.0f;
+    const f3 d = normalize(mk3(tg[0], tg[1], tg[2]) / tg[3]);
+    const float* V = sd.inverseView;
+    float wd[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) wd[r] = V[0 * 4 + r] * d.x + V[1 * 4 + r] * d.y + V[2 * 4 + r] * d.z + V[3 * 4 + r] * 0.0f;
+    return normalize(mk3(wd[0], wd[1], wd[2]));
+}
+
+/* Wave-level sum of a per-lane u32 counter, one u64 atomic per wave. */
+__device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v)
+{
+    unsigned long long s = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
+}
+
+} // namespace dev
+} // namespace wcpt
+
+#endif /* WCPT_PT_DEVICE_H */

@@ -1,0 +1,147 @@
+/*
+ * pt_kernels.hip — the path-tracing megakernel for gfx950 (reference: src/shaders/pathTracer.comp:286-324).
+ *
+ * Launch shape: one 64-lane wave per 8x8 pixel tile (the reference's 4x4 = 16-invocation workgroups would
+ * leave 48 of 64 lanes idle on wave64 CDNA). A bounds guard makes any width/height legal (the reference
+ * has none, :289). SceneData arrives by value in the kernarg segment.
+ */
+#include <hip/hip_runtime.h>
+
+#include "pt_device.h"
+#include "pt_kernels.h"
+
+namespace wcpt {
+namespace dev {
+
+/* Pixel tile -> block mapping. Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+ * "Workgroup dispatch"); remapping the linear block id so that each XCD walks a contiguous band of tiles
+ * keeps neighbouring (coherent) tiles on one XCD's L2. Speed only; any placement is correct. */
+__device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTotal, uint32_t& tx, uint32_t& ty)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t per = (tilesTotal + 7u) / 8u;
+    const uint32_t xcd = b & 7u, k = b >> 3;
+    uint32_t t = xcd * per + k;
+    if (t >= tilesTotal || (tilesTotal & 7u) != 0u) t = b; /* exact band split only when divisible by 8 */
+    tx = t % tilesX;
+    ty = t / tilesX;
+}
+
+template <bool COUNT, int STACK>
+__global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
+                                                    const wcpt_sphere* __restrict__ spheres,
+                                                    const wcpt_draw_command* __restrict__ draws,
+                                                    float4* __restrict__ image, uint32_t W, uint32_t H, uint32_t y0,
+                                                    uint32_t rows, uint32_t tilesX, uint32_t tilesTotal,
+                                                    uint32_t* __restrict__ status,
+                                                    unsigned long long* __restrict__ counters)
+{
+    uint32_t tx, ty;
+    tile_of_block(tilesX, tilesTotal, tx, ty);
+    const uint32_t lx = tx * 8u + (threadIdx.x & 7u);
+    const uint32_t ly = ty * 8u + (threadIdx.x >> 3);
+    const bool active = lx < W && ly < rows;
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool overflow = false;
+    if (active) {
+        const uint32_t x = lx, y = y0 + ly;
+        const f3 dir = primary_direction(sd, x, y, W, H);
+        const uint32_t pixel_index = x + y * W + sd.renderedFramesCount * 719393u; /* :304 */
+        uint32_t seed = pcg_hash(pixel_index);
+        PrivateStack<STACK> stk;
+        f3 result = mk3(0.0f, 0.0f, 0.0f);
+        const f3 origin = mk3(sd.position[0], sd.position[1], sd.position[2]);
+        for (uint32_t s = 0; s < sd.samples; s++) { /* :309-310, all samples share the primary ray */
+            Ray r;
+            r.origin = origin;
+            r.direction = dir;
+            r.invDirection = rcp3(dir);
+            result = result + TraceRay<COUNT, STACK>(r, seed, sd, mats, spheres, draws, stk, cnt, overflow);
+        }
+        result = result / (float)sd.samples; /* :312 */
+        if (!COUNT) {
+            float4* px = image + (size_t)ly * W + lx;
+            f3 acc;
+            if (sd.renderedFramesCount == 0) { /* :318 — the loaded value would be discarded */
+                acc = result;
+            } else {
+                const float4 o = *px;                                          /* :314 */
+                const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u); /* :316 */
+                const float iw = 1.0f - weight;
+                acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight, o.z * iw + result.z * weight);
+            }
+            *px = make_float4(acc.x, acc.y, acc.z, 1.0f);                     /* :323 */
+        }
+        if (COUNT) cnt.pixels = 1;
+    }
+    if (overflow) atomicOr(status, 1u);
+    if (COUNT) {
+        wave_add_u64(&counters[0], cnt.pixels);
+        wave_add_u64(&counters[1], cnt.segments);
+        wave_add_u64(&counters[2], cnt.sphere_tests);
+        wave_add_u64(&counters[3], cnt.node_pops);
+        wave_add_u64(&counters[4], cnt.interior_visits);
+        wave_add_u64(&counters[5], cnt.triangle_tests);
+        wave_add_u64(&counters[6], cnt.hits);
+        wave_add_u64(&counters[7], cnt.draw_fetches);
+    }
+}
+
+/* Device self-tests: evaluate the device definitions of the RNG and the deterministic libm on host inputs. */
+__global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __restrict__ in, const uint32_t* __restrict__ in2,
+                                                   uint32_t* __restrict__ out, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t a = in[i];
+    switch (fn) {
+    case 0: out[i] = pcg_hash(a); break;
+    case 1: {
+        uint32_t s = a;
+        for (int k = 0; k < 4; k++) out[4u * i + (uint32_t)k] = __float_as_uint(rand_f(s));
+        break;
+    }
+    case 2: out[i] = __float_as_uint(wcpt_logf(__uint_as_float(a))); break;
+    case 3: out[i] = __float_as_uint(wcpt_cosf(__uint_as_float(a))); break;
+    case 4: out[i] = __float_as_uint(wcpt_expf(__uint_as_float(a))); break;
+    case 5: out[i] = __float_as_uint(sqrtf(__uint_as_float(a))); break;
+    case 6: out[i] = __float_as_uint(__uint_as_float(a) / __uint_as_float(in2[i])); break;
+    case 7: { /* RandomDirection: 3 words per input */
+        uint32_t s = a;
+        const f3 d = RandomDirection(s);
+        out[3u * i + 0u] = __float_as_uint(d.x);
+        out[3u * i + 1u] = __float_as_uint(d.y);
+        out[3u * i + 2u] = __float_as_uint(d.z);
+        break;
+    }
+    default: break;
+    }
+}
+
+} // namespace dev
+
+/* ------------------------------------------------------------------------------------------------ */
+hipError_t launch_megakernel(const LaunchArgs& a, bool count, hipStream_t stream)
+{
+    const uint32_t tilesX = (a.W + 7u) / 8u;
+    const uint32_t tilesY = (a.rows + 7u) / 8u;
+    const uint32_t tiles = tilesX * tilesY;
+    if (tiles == 0) return hipSuccess;
+    const dim3 grid(tiles), block(64);
+    if (count)
+        hipLaunchKernelGGL((dev::pt_megakernel<true, kStackDepth>), grid, block, 0, stream, a.sd, a.materials, a.spheres,
+                           a.draws, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
+    else
+        hipLaunchKernelGGL((dev::pt_megakernel<false, kStackDepth>), grid, block, 0, stream, a.sd, a.materials, a.spheres,
+                           a.draws, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::pt_selftest, dim3((n + 255u) / 256u), dim3(256), 0, stream, fn, in, in2, out, n);
+    return hipGetLastError();
+}
+
+} // namespace wcpt

@@ -1,0 +1,559 @@
+/*
+ * wcpt_runtime.hip — C-ABI runtime: device context, device buffers, output image, dispatch, timing.
+ *
+ * Replaces the Vulkan plumbing of the reference's renderer host (src/PathTracingRenderer.jai,
+ * src/BufferManager.jai, modules/VKUtils/{Buffer,Synchronization}.jai); see include/wcpt.h for the
+ * line-by-line mapping. HIP device memory replaces VMA GPU-only buffers; a device pointer IS the buffer
+ * device address (VK_KHR_buffer_device_address, pathTracer.comp:74-95).
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/wcpt.h"
+#include "pt_kernels.h"
+
+namespace {
+
+std::mutex g_err_mutex;
+std::string g_last_error;
+
+struct Buffer {
+    void* ptr = nullptr;
+    uint64_t bytes = 0;
+};
+
+} // namespace
+
+struct wcpt_context {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::unordered_map<uint64_t, Buffer> buffers;
+    uint64_t next_handle = 1;
+    float4* image = nullptr;           /* the image kernels write: own_image or an external buffer */
+    float4* own_image = nullptr;
+    uint64_t image_bytes_cap = 0;
+    uint64_t external_bytes = 0;       /* != 0 while an external image is attached */
+    uint32_t width = 0, height = 0, y0 = 0, rows = 0; /* rows == height when not sharded */
+    bool sharded = false;
+    uint32_t* d_status = nullptr;
+    unsigned long long* d_counters = nullptr;
+    uint32_t* d_scratch = nullptr;
+    uint64_t scratch_bytes = 0;
+    int kernel = WCPT_KERNEL_MEGAKERNEL;
+    std::string last_error;
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    size_t events_used = 0;
+};
+
+namespace {
+
+int set_error(wcpt_context* ctx, int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->last_error = buf;
+    std::lock_guard<std::mutex> lk(g_err_mutex);
+    g_last_error = buf;
+    return code;
+}
+
+int hip_fail(wcpt_context* ctx, hipError_t e, const char* what)
+{
+    const int code = (e == hipErrorOutOfMemory) ? WCPT_ERROR_OUT_OF_DEVICE_MEMORY : WCPT_ERROR_DEVICE_LOST;
+    return set_error(ctx, code, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr, what)                                  \
+    do {                                                          \
+        hipError_t _e = (expr);                                   \
+        if (_e != hipSuccess) return hip_fail((ctx), _e, (what)); \
+    } while (0)
+
+int bind(wcpt_context* ctx)
+{
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    HIP_TRY(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    return WCPT_SUCCESS;
+}
+
+Buffer* find_buffer(wcpt_context* ctx, wcpt_buffer h)
+{
+    auto it = ctx->buffers.find(h);
+    return it == ctx->buffers.end() ? nullptr : &it->second;
+}
+
+int ensure_scratch(wcpt_context* ctx, uint64_t bytes)
+{
+    if (ctx->scratch_bytes >= bytes) return WCPT_SUCCESS;
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    ctx->d_scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    HIP_TRY(ctx, hipMalloc(&ctx->d_scratch, bytes), "hipMalloc(selftest scratch)");
+    ctx->scratch_bytes = bytes;
+    return WCPT_SUCCESS;
+}
+
+int alloc_image(wcpt_context* ctx, uint32_t w, uint32_t h, uint32_t y0, uint32_t rows)
+{
+    const uint64_t bytes = (uint64_t)w * rows * 16ull;
+    if (ctx->external_bytes) {
+        if (bytes > ctx->external_bytes)
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "external image of %llu bytes < %llu needed",
+                             (unsigned long long)ctx->external_bytes, (unsigned long long)bytes);
+    } else if (bytes > ctx->image_bytes_cap) {
+        if (ctx->own_image) (void)hipFree(ctx->own_image);
+        ctx->own_image = nullptr;
+        ctx->image = nullptr;
+        ctx->image_bytes_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&ctx->own_image, bytes), "hipMalloc(image)");
+        ctx->image_bytes_cap = bytes;
+        ctx->image = ctx->own_image;
+    }
+    ctx->width = w;
+    ctx->height = h;
+    ctx->y0 = y0;
+    ctx->rows = rows;
+    return WCPT_SUCCESS;
+}
+
+int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                  uint64_t draws, bool count)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!scene) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: null SceneData");
+    if (!ctx->image || ctx->width == 0 || ctx->rows == 0)
+        return set_error(ctx, WCPT_ERROR_NO_SCREEN, "wcpt_render: no output image (call wcpt_create_screen)");
+    if (scene->sphereCount > 0 && spheres == 0)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: sphereCount > 0 with a null sphere buffer");
+    if (scene->drawCommandCount > 0 && draws == 0)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: drawCommandCount > 0 with null draw commands");
+    if (materials == 0 && (scene->sphereCount > 0 || scene->drawCommandCount > 0))
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: null material buffer");
+    wcpt::LaunchArgs a;
+    a.sd = *scene;
+    a.materials = reinterpret_cast<const wcpt_material*>(materials);
+    a.spheres = reinterpret_cast<const wcpt_sphere*>(spheres);
+    a.draws = reinterpret_cast<const wcpt_draw_command*>(draws);
+    a.image = ctx->image;
+    a.W = ctx->width;
+    a.H = ctx->height;
+    a.y0 = ctx->y0;
+    a.rows = ctx->rows;
+    a.status = ctx->d_status;
+    a.counters = ctx->d_counters;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ctx->profiling && !count) {
+        if (ctx->events_used == ctx->events.size()) {
+            hipEvent_t b, c;
+            HIP_TRY(ctx, hipEventCreate(&b), "hipEventCreate");
+            HIP_TRY(ctx, hipEventCreate(&c), "hipEventCreate");
+            ctx->events.emplace_back(b, c);
+        }
+        e0 = ctx->events[ctx->events_used].first;
+        e1 = ctx->events[ctx->events_used].second;
+        ctx->events_used++;
+        HIP_TRY(ctx, hipEventRecord(e0, ctx->stream), "hipEventRecord");
+    }
+    hipError_t e = hipSuccess;
+    switch (ctx->kernel) {
+    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, count, ctx->stream); break;
+    default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
+    if (e1) HIP_TRY(ctx, hipEventRecord(e1, ctx->stream), "hipEventRecord");
+    return WCPT_SUCCESS;
+}
+
+int read_status(wcpt_context* ctx)
+{
+    uint32_t st = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status, 4, hipMemcpyDeviceToHost, ctx->stream), "hipMemcpyAsync(status)");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (st) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0, 4, ctx->stream), "hipMemsetAsync(status)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+        return set_error(ctx, WCPT_ERROR_STACK_OVERFLOW,
+                         "BVH traversal stack overflow (tree deeper than %d levels); image is incomplete",
+                         wcpt::kStackDepth);
+    }
+    return WCPT_SUCCESS;
+}
+
+} // namespace
+
+extern "C" {
+
+int wcpt_abi_version(void) { return WCPT_ABI_VERSION; }
+
+const char* wcpt_last_error(const wcpt_context* ctx)
+{
+    if (ctx) return ctx->last_error.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mutex);
+    return g_last_error.c_str();
+}
+
+int wcpt_device_count(int* count)
+{
+    if (!count) return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        (void)hipGetLastError();
+        return WCPT_SUCCESS; /* no device is not an error for the query */
+    }
+    *count = n;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_create(int device, wcpt_context** out_ctx)
+{
+    if (!out_ctx) return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "null out_ctx");
+    *out_ctx = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return set_error(nullptr, WCPT_ERROR_INITIALIZATION_FAILED, "no HIP device available");
+    }
+    if (device < 0 || device >= n)
+        return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "device %d out of range [0,%d)", device, n);
+    wcpt_context* ctx = new (std::nothrow) wcpt_context();
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_OUT_OF_HOST_MEMORY, "out of host memory");
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_status, 4);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_counters, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 4);
+    if (e != hipSuccess) {
+        int rc = hip_fail(nullptr, e, "wcpt_create");
+        wcpt_destroy(ctx);
+        return rc;
+    }
+    ctx->stream = ctx->own_stream;
+    *out_ctx = ctx;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_destroy(wcpt_context* ctx)
+{
+    if (!ctx) return WCPT_SUCCESS;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->buffers)
+        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    if (ctx->own_image) (void)hipFree(ctx->own_image);
+    if (ctx->d_status) (void)hipFree(ctx->d_status);
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    for (auto& p : ctx->events) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_set_stream(wcpt_context* ctx, void* hip_stream)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_set_kernel(wcpt_context* ctx, int variant)
+{
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    if (variant != WCPT_KERNEL_MEGAKERNEL)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", variant);
+    ctx->kernel = variant;
+    return WCPT_SUCCESS;
+}
+
+/* ---- buffers ------------------------------------------------------------------------------------ */
+int wcpt_buffer_alloc(wcpt_context* ctx, uint64_t bytes, wcpt_buffer* out)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!out) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null out handle");
+    Buffer b;
+    b.bytes = bytes;
+    if (bytes) HIP_TRY(ctx, hipMalloc(&b.ptr, bytes), "hipMalloc(buffer)");
+    const uint64_t h = ctx->next_handle++;
+    ctx->buffers[h] = b;
+    *out = h;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_buffer_upload(wcpt_context* ctx, wcpt_buffer buf, const void* src, uint64_t bytes, uint64_t offset)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    Buffer* b = find_buffer(ctx, buf);
+    if (!b) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle %llu", (unsigned long long)buf);
+    if (bytes && !src) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null upload source");
+    if (offset + bytes > b->bytes) {
+        /* grow, keeping the old contents (BufferManager.jai:53-54 reallocates on growth) */
+        void* np = nullptr;
+        HIP_TRY(ctx, hipMalloc(&np, offset + bytes), "hipMalloc(buffer grow)");
+        if (b->ptr && b->bytes) {
+            hipError_t e = hipMemcpyAsync(np, b->ptr, b->bytes, hipMemcpyDeviceToDevice, ctx->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) {
+                (void)hipFree(np);
+                return hip_fail(ctx, e, "buffer grow copy");
+            }
+            (void)hipFree(b->ptr);
+        }
+        b->ptr = np;
+        b->bytes = offset + bytes;
+    }
+    if (bytes) {
+        HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(b->ptr) + offset, src, bytes, hipMemcpyHostToDevice, ctx->stream),
+                "hipMemcpyAsync(upload)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(upload)"); /* blocking, like :98-112 */
+    }
+    return WCPT_SUCCESS;
+}
+
+int wcpt_buffer_download(wcpt_context* ctx, wcpt_buffer buf, void* dst, uint64_t bytes, uint64_t offset)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    Buffer* b = find_buffer(ctx, buf);
+    if (!b) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle %llu", (unsigned long long)buf);
+    if (offset + bytes > b->bytes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "download out of range");
+    if (bytes && !dst) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null download destination");
+    if (bytes) {
+        HIP_TRY(ctx, hipMemcpyAsync(dst, static_cast<char*>(b->ptr) + offset, bytes, hipMemcpyDeviceToHost, ctx->stream),
+                "hipMemcpyAsync(download)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(download)");
+    }
+    return WCPT_SUCCESS;
+}
+
+int wcpt_buffer_size(wcpt_context* ctx, wcpt_buffer buf, uint64_t* out_bytes)
+{
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    Buffer* b = find_buffer(ctx, buf);
+    if (!b) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle");
+    if (!out_bytes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null out_bytes");
+    *out_bytes = b->bytes;
+    return WCPT_SUCCESS;
+}
+
+uint64_t wcpt_buffer_device_address(wcpt_context* ctx, wcpt_buffer buf)
+{
+    if (!ctx) return 0;
+    Buffer* b = find_buffer(ctx, buf);
+    if (!b) {
+        set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle");
+        return 0;
+    }
+    return reinterpret_cast<uint64_t>(b->ptr);
+}
+
+int wcpt_buffer_free(wcpt_context* ctx, wcpt_buffer buf)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    auto it = ctx->buffers.find(buf);
+    if (it == ctx->buffers.end()) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(free)");
+    if (it->second.ptr) HIP_TRY(ctx, hipFree(it->second.ptr), "hipFree");
+    ctx->buffers.erase(it);
+    return WCPT_SUCCESS;
+}
+
+/* ---- image -------------------------------------------------------------------------------------- */
+int wcpt_create_screen(wcpt_context* ctx, uint32_t width, uint32_t height)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (width == 0 || height == 0) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "zero-sized screen");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    uint32_t y0 = 0, rows = height;
+    if (ctx->sharded && ctx->y0 < height) {
+        y0 = ctx->y0;
+        rows = (ctx->y0 + ctx->rows <= height) ? ctx->rows : height - ctx->y0;
+    } else {
+        ctx->sharded = false;
+    }
+    return alloc_image(ctx, width, height, y0, rows);
+}
+
+int wcpt_resize(wcpt_context* ctx, uint32_t width, uint32_t height)
+{
+    return wcpt_create_screen(ctx, width, height); /* Resize = DestroyScreen + CreateScreen (:393-397) */
+}
+
+int wcpt_set_row_range(wcpt_context* ctx, uint32_t y0, uint32_t rows)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (rows == 0) {
+        ctx->sharded = false;
+        if (ctx->height) return alloc_image(ctx, ctx->width, ctx->height, 0, ctx->height);
+        return WCPT_SUCCESS;
+    }
+    if (ctx->height && (uint64_t)y0 + rows > ctx->height)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "row range [%u,%u) outside frame height %u", y0, y0 + rows,
+                         ctx->height);
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    ctx->sharded = true;
+    ctx->y0 = y0;
+    ctx->rows = rows;
+    if (ctx->height) return alloc_image(ctx, ctx->width, ctx->height, y0, rows);
+    return WCPT_SUCCESS;
+}
+
+uint64_t wcpt_image_device_ptr(wcpt_context* ctx) { return ctx ? reinterpret_cast<uint64_t>(ctx->image) : 0; }
+
+int wcpt_set_external_image(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (device_ptr == 0) {
+        ctx->external_bytes = 0;
+        ctx->image = ctx->own_image;
+        if (ctx->width && ctx->rows) return alloc_image(ctx, ctx->width, ctx->height, ctx->y0, ctx->rows);
+        return WCPT_SUCCESS;
+    }
+    if (bytes == 0) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "external image of 0 bytes");
+    if (ctx->width && (uint64_t)ctx->width * ctx->rows * 16ull > bytes)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "external image too small for %ux%u", ctx->width, ctx->rows);
+    ctx->external_bytes = bytes;
+    ctx->image = reinterpret_cast<float4*>(device_ptr);
+    return WCPT_SUCCESS;
+}
+
+int wcpt_readback(wcpt_context* ctx, float* dst, uint64_t bytes)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    const uint64_t have = (uint64_t)ctx->width * ctx->rows * 16ull;
+    if (!ctx->image) return set_error(ctx, WCPT_ERROR_NO_SCREEN, "no output image");
+    if (!dst || bytes > have) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "readback of %llu bytes, image holds %llu",
+                                               (unsigned long long)bytes, (unsigned long long)have);
+    HIP_TRY(ctx, hipMemcpyAsync(dst, ctx->image, bytes, hipMemcpyDeviceToHost, ctx->stream), "hipMemcpyAsync(readback)");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(readback)");
+    return read_status(ctx);
+}
+
+int wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    const uint64_t have = (uint64_t)ctx->width * ctx->rows * 16ull;
+    if (!ctx->image) return set_error(ctx, WCPT_ERROR_NO_SCREEN, "no output image");
+    if (!src || bytes > have) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "image upload size");
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->image, src, bytes, hipMemcpyHostToDevice, ctx->stream), "hipMemcpyAsync(image)");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    return WCPT_SUCCESS;
+}
+
+/* ---- dispatch ------------------------------------------------------------------------------------ */
+int wcpt_render(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                uint64_t draw_commands)
+{
+    return render_common(ctx, scene, materials, spheres, draw_commands, false);
+}
+
+int wcpt_sync(wcpt_context* ctx)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    return read_status(ctx);
+}
+
+int wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                         uint64_t draw_commands, wcpt_counters* out)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!out) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null counters");
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), ctx->stream), "hipMemsetAsync");
+    rc = render_common(ctx, scene, materials, spheres, draw_commands, true);
+    if (rc) return rc;
+    unsigned long long h[8];
+    HIP_TRY(ctx, hipMemcpyAsync(h, ctx->d_counters, sizeof(h), hipMemcpyDeviceToHost, ctx->stream), "hipMemcpyAsync");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    out->pixels = h[0];
+    out->segments = h[1];
+    out->sphere_tests = h[2];
+    out->node_pops = h[3];
+    out->interior_visits = h[4];
+    out->triangle_tests = h[5];
+    out->hits = h[6];
+    out->draw_fetches = h[7];
+    return read_status(ctx);
+}
+
+/* ---- timing --------------------------------------------------------------------------------------- */
+int wcpt_profile_begin(wcpt_context* ctx)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    ctx->profiling = true;
+    ctx->events_used = 0;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_profile_end(wcpt_context* ctx, double* kernel_ms_total, uint32_t* launches)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    double total = 0.0;
+    for (size_t i = 0; i < ctx->events_used; i++) {
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->events[i].first, ctx->events[i].second), "hipEventElapsedTime");
+        total += ms;
+    }
+    if (kernel_ms_total) *kernel_ms_total = total;
+    if (launches) *launches = (uint32_t)ctx->events_used;
+    ctx->profiling = false;
+    ctx->events_used = 0;
+    return WCPT_SUCCESS;
+}
+
+/* ---- self-test -------------------------------------------------------------------------------------- */
+int wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!in || !out || (fn == 6 && !in2)) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
+    if (fn < 0 || fn > 7) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
+    const uint64_t outw = (fn == 1) ? 4ull * n : (fn == 7 ? 3ull * n : (uint64_t)n);
+    rc = ensure_scratch(ctx, (2ull * n + outw) * 4ull + 16);
+    if (rc) return rc;
+    uint32_t* d_in = ctx->d_scratch;
+    uint32_t* d_in2 = d_in + n;
+    uint32_t* d_out = d_in2 + n;
+    HIP_TRY(ctx, hipMemcpyAsync(d_in, in, 4ull * n, hipMemcpyHostToDevice, ctx->stream), "selftest upload");
+    if (in2) HIP_TRY(ctx, hipMemcpyAsync(d_in2, in2, 4ull * n, hipMemcpyHostToDevice, ctx->stream), "selftest upload");
+    HIP_TRY(ctx, wcpt::launch_selftest(fn, d_in, d_in2, d_out, n, ctx->stream), "selftest launch");
+    HIP_TRY(ctx, hipMemcpyAsync(out, d_out, 4ull * outw, hipMemcpyDeviceToHost, ctx->stream), "selftest download");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    return WCPT_SUCCESS;
+}
+
+} /* extern "C" */

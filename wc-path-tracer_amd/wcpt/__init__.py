@@ -1,0 +1,24 @@
+"""wcpt — MI355X-native path-tracing compute path (drop-in for pathTracer.comp of myri4/WC-Path-tracer).
+
+The compute lives in libwcpt.so (hand-written HIP for gfx950 behind the C-ABI of include/wcpt.h); this
+package is the Python host mirror used by tests and the benchmark.
+"""
+from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL, KERNEL_PERSISTENT,
+                   KERNEL_WAVEFRONT, LIB_PATH, MATERIAL_DIELECTRIC, MATERIAL_DTYPE, MATERIAL_METAL, NODE_DTYPE,
+                   SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, WcptError, lib)
+from .renderer import Context, DeviceScene, PathTracingRenderer
+from . import scene
+
+__all__ = [
+    "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL", "KERNEL_PERSISTENT",
+    "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
+    "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
+    "PathTracingRenderer", "scene", "device_count",
+]
+
+
+def device_count() -> int:
+    import ctypes as C
+    n = C.c_int()
+    lib.wcpt_device_count(C.byref(n))
+    return n.value

@@ -1,0 +1,165 @@
+"""ctypes binding of libwcpt.so (the C-ABI declared in include/wcpt.h).
+
+The shared library is built in-tree (``make -C wc-path-tracer_amd``) and lives next to this package. There
+is no fallback: if the library is missing, importing :mod:`wcpt` raises, so nothing can silently run a
+non-HIP path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libwcpt.so")
+
+WCPT_SUCCESS = 0
+ERRORS = {
+    -1: "WCPT_ERROR_OUT_OF_HOST_MEMORY",
+    -2: "WCPT_ERROR_OUT_OF_DEVICE_MEMORY",
+    -3: "WCPT_ERROR_INITIALIZATION_FAILED",
+    -4: "WCPT_ERROR_DEVICE_LOST",
+    -13: "WCPT_ERROR_UNKNOWN",
+    -1000: "WCPT_ERROR_INVALID_ARGUMENT",
+    -1001: "WCPT_ERROR_INVALID_HANDLE",
+    -1002: "WCPT_ERROR_STACK_OVERFLOW",
+    -1003: "WCPT_ERROR_NO_SCREEN",
+    -1004: "WCPT_ERROR_PARSE",
+}
+WCPT_ERROR_INVALID_ARGUMENT = -1000
+WCPT_ERROR_INVALID_HANDLE = -1001
+WCPT_ERROR_STACK_OVERFLOW = -1002
+WCPT_ERROR_NO_SCREEN = -1003
+
+MATERIAL_METAL = 0
+MATERIAL_DIELECTRIC = 1
+
+KERNEL_MEGAKERNEL = 0
+KERNEL_PERSISTENT = 1
+KERNEL_WAVEFRONT = 2
+
+# ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
+SCENE_DATA_DTYPE = np.dtype([
+    ("inverseProjection", "<f4", (16,)), ("inverseView", "<f4", (16,)), ("position", "<f4", (3,)),
+    ("maxBounceCount", "<u4"), ("samples", "<u4"), ("sphereCount", "<u4"), ("drawCommandCount", "<u4"),
+    ("renderedFramesCount", "<u4"), ("boxID", "<u4")])
+MATERIAL_DTYPE = np.dtype([
+    ("type", "<u4"), ("albedo", "<f4", (3,)), ("emission", "<f4", (3,)), ("emissionStrength", "<f4"),
+    ("metallic", "<f4"), ("roughness", "<f4"), ("absorption", "<f4", (3,)), ("absorptionStrength", "<f4"),
+    ("ior", "<f4")])
+SPHERE_DTYPE = np.dtype([("position", "<f4", (3,)), ("radius", "<f4"), ("material", "<u4")])
+NODE_DTYPE = np.dtype([("min", "<f4", (3,)), ("max", "<f4", (3,)), ("leftNodeOrTriangleIndex", "<u4"),
+                       ("triangleCount", "<u4")])
+DRAW_COMMAND_DTYPE = np.dtype([("vertexBuffer", "<u8"), ("indexBuffer", "<u8"), ("bvhBuffer", "<u8"),
+                               ("indexCount", "<u4"), ("_pad", "<u4")])
+COUNTER_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",
+                  "hits", "draw_fetches")
+assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
+assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
+
+
+class Counters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in COUNTER_FIELDS}
+
+
+class Mesh(C.Structure):
+    _fields_ = [("positions", C.POINTER(C.c_float)), ("vertex_count", C.c_uint32),
+                ("indices", C.POINTER(C.c_uint32)), ("index_count", C.c_uint32)]
+
+
+class Camera(C.Structure):
+    """PathTracingRenderer.jai:6-20 (matrices column-major, as the shader reads them)."""
+    _fields_ = [("position", C.c_float * 3), ("direction", C.c_float * 3), ("yaw", C.c_float),
+                ("pitch", C.c_float), ("fov", C.c_float), ("projection", C.c_float * 16),
+                ("view", C.c_float * 16), ("inverseProjection", C.c_float * 16),
+                ("inverseView", C.c_float * 16)]
+
+
+class SceneC(C.Structure):
+    _fields_ = [("mesh", Mesh), ("materials", C.c_void_p), ("material_count", C.c_uint32),
+                ("spheres", C.c_void_p), ("sphere_count", C.c_uint32), ("camera", Camera)]
+
+
+_p = C.c_void_p
+_u32 = C.c_uint32
+_u64 = C.c_uint64
+_i = C.c_int
+
+_PROTOTYPES = {
+    "wcpt_abi_version": (_i, []),
+    "wcpt_device_count": (_i, [C.POINTER(_i)]),
+    "wcpt_create": (_i, [_i, C.POINTER(_p)]),
+    "wcpt_destroy": (_i, [_p]),
+    "wcpt_last_error": (C.c_char_p, [_p]),
+    "wcpt_set_stream": (_i, [_p, _p]),
+    "wcpt_set_kernel": (_i, [_p, _i]),
+    "wcpt_buffer_alloc": (_i, [_p, _u64, C.POINTER(_u64)]),
+    "wcpt_buffer_upload": (_i, [_p, _u64, _p, _u64, _u64]),
+    "wcpt_buffer_download": (_i, [_p, _u64, _p, _u64, _u64]),
+    "wcpt_buffer_size": (_i, [_p, _u64, C.POINTER(_u64)]),
+    "wcpt_buffer_device_address": (_u64, [_p, _u64]),
+    "wcpt_buffer_free": (_i, [_p, _u64]),
+    "wcpt_create_screen": (_i, [_p, _u32, _u32]),
+    "wcpt_resize": (_i, [_p, _u32, _u32]),
+    "wcpt_set_row_range": (_i, [_p, _u32, _u32]),
+    "wcpt_image_device_ptr": (_u64, [_p]),
+    "wcpt_set_external_image": (_i, [_p, _u64, _u64]),
+    "wcpt_readback": (_i, [_p, _p, _u64]),
+    "wcpt_image_upload": (_i, [_p, _p, _u64]),
+    "wcpt_render": (_i, [_p, _p, _u64, _u64, _u64]),
+    "wcpt_sync": (_i, [_p]),
+    "wcpt_render_counters": (_i, [_p, _p, _u64, _u64, _u64, C.POINTER(Counters)]),
+    "wcpt_profile_begin": (_i, [_p]),
+    "wcpt_profile_end": (_i, [_p, C.POINTER(C.c_double), C.POINTER(_u32)]),
+    "wcpt_obj_parse": (_i, [C.c_char_p, _u64, C.POINTER(Mesh)]),
+    "wcpt_obj_load": (_i, [C.c_char_p, C.POINTER(Mesh)]),
+    "wcpt_mesh_free": (None, [C.POINTER(Mesh)]),
+    "wcpt_bvh_build": (_i, [_p, _u32, _p, _u32, _p, _u32, C.POINTER(_u32)]),
+    "wcpt_camera_update": (_i, [C.POINTER(Camera), C.c_float]),
+    "wcpt_scene_generate": (_i, [C.c_char_p, _u32, C.POINTER(SceneC)]),
+    "wcpt_scene_free": (None, [C.POINTER(SceneC)]),
+    "wcpt_mesh_to_obj": (_i, [C.POINTER(Mesh), C.POINTER(C.c_void_p), C.POINTER(_u64)]),
+    "wcpt_string_free": (None, [C.c_void_p]),
+    "wcpt_selftest_device": (_i, [_p, _i, _p, _p, _p, _u32]),
+}
+
+EXPORTED_SYMBOLS = tuple(_PROTOTYPES)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libwcpt.so not found at {LIB_PATH}: build it with `make -C wc-path-tracer_amd` "
+            "(or __graft_entry__.build()). There is no non-HIP fallback.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class WcptError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {message}")
+        self.code = code
+
+
+def check(rc: int, ctx=None):
+    if rc != WCPT_SUCCESS:
+        msg = lib.wcpt_last_error(ctx)
+        raise WcptError(rc, msg.decode(errors="replace") if msg else "")
+    return rc
+
+
+def ptr(a: np.ndarray) -> int:
+    """Raw address of a C-contiguous numpy array."""
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data
