@@ -163,8 +163,9 @@ def test_full_size_rows_vs_oracle(gpu_ctx):
 
 def test_deterministic_repeat(gpu_ctx):
     s = get_scene("atrium")
-    a, ca = gpu_render(gpu_ctx, s, 160, 90, bounces=4, frame=2)
-    b, cb = gpu_render(gpu_ctx, s, 160, 90, bounces=4, frame=2)
+    init = np.full((90, 160, 4), 0.25, np.float32)
+    a, ca = gpu_render(gpu_ctx, s, 160, 90, bounces=4, frame=2, init=init)
+    b, cb = gpu_render(gpu_ctx, s, 160, 90, bounces=4, frame=2, init=init)
     assert np.array_equal(a, b) and ca == cb
 
 

@@ -162,10 +162,7 @@ class DeviceScene:
         self.spheres = self._buf(scene.spheres)
         draws = np.zeros(len(scene.meshes), dtype=DRAW_COMMAND_DTYPE)
         for i, m in enumerate(scene.meshes):
-            vb = self._buf(m.positions)
-            ib = self._buf(m.indices)
-            nb = self._buf(m.nodes)
-            draws[i] = (ctx.buffer_address(vb), ctx.buffer_address(ib), ctx.buffer_address(nb), m.indices.size, 0)
+            draws[i] = (self._buf(m.positions), self._buf(m.indices), self._buf(m.nodes), m.indices.size, 0)
         self.draws = self._buf(draws)
 
     def _buf(self, arr: np.ndarray) -> int:
