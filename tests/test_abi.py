@@ -1,0 +1,94 @@
+"""The C-ABI surface (no GPU compute): the library loads, exports every symbol include/wcpt.h declares, keeps the
+reference byte layouts, and fails with error codes (never aborts) when no device is present."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import wcpt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "wcpt.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(wcpt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    names = declared_functions()
+    assert len(names) >= 30
+    lib = C.CDLL(wcpt.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(wcpt.EXPORTED_SYMBOLS), set(names) ^ set(wcpt.EXPORTED_SYMBOLS)
+
+
+def test_abi_version():
+    assert wcpt.lib.wcpt_abi_version() == 1
+
+
+def test_layouts_match_reference():
+    """GLSL scalar layouts (pathTracer.comp:10-95) == Jai structs (PathTracingRenderer.jai:38-140)."""
+    sd = wcpt.SCENE_DATA_DTYPE
+    assert sd.itemsize == 164
+    assert [sd.fields[n][1] for n in ("inverseProjection", "inverseView", "position", "maxBounceCount",
+                                      "samples", "sphereCount", "drawCommandCount", "renderedFramesCount",
+                                      "boxID")] == [0, 64, 128, 140, 144, 148, 152, 156, 160]
+    m = wcpt.MATERIAL_DTYPE
+    assert m.itemsize == 60
+    assert [m.fields[n][1] for n in m.names] == [0, 4, 16, 28, 32, 36, 40, 52, 56]
+    assert wcpt.SPHERE_DTYPE.itemsize == 20 and wcpt.NODE_DTYPE.itemsize == 32
+    assert wcpt.DRAW_COMMAND_DTYPE.itemsize == 32
+    assert [wcpt.DRAW_COMMAND_DTYPE.fields[n][1] for n in wcpt.DRAW_COMMAND_DTYPE.names] == [0, 8, 16, 24, 28]
+
+
+def test_header_compiles_as_c_with_layout_asserts(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text(f'''#include "{HEADER}"
+#include <stddef.h>
+_Static_assert(sizeof(wcpt_scene_data) == 164, "SceneData");
+_Static_assert(offsetof(wcpt_scene_data, renderedFramesCount) == 156, "frames");
+_Static_assert(sizeof(wcpt_material) == 60, "Material");
+_Static_assert(offsetof(wcpt_material, ior) == 56, "ior");
+_Static_assert(sizeof(wcpt_sphere) == 20, "Sphere");
+_Static_assert(sizeof(wcpt_node) == 32, "Node");
+_Static_assert(sizeof(wcpt_draw_command) == 32, "DrawCommand");
+int main(void) {{ return 0; }}
+''')
+    rc = os.system(f"gcc -std=c99 -Wall -Werror -c {src} -o {tmp_path / 't.o'}")
+    assert rc == 0
+
+
+@pytest.mark.skipif(wcpt.device_count() > 0, reason="checks the no-device error path")
+def test_no_device_errors_cleanly():
+    h = C.c_void_p()
+    rc = wcpt.lib.wcpt_create(0, C.byref(h))
+    assert rc == -3 and not h.value                         # WCPT_ERROR_INITIALIZATION_FAILED
+    assert b"no HIP device" in wcpt.lib.wcpt_last_error(None)
+    with pytest.raises(wcpt.WcptError):
+        wcpt.Context(0)
+
+
+def test_null_handles_rejected():
+    assert wcpt.lib.wcpt_render(None, None, 0, 0, 0) == -1001
+    assert wcpt.lib.wcpt_sync(None) == -1001
+    assert wcpt.lib.wcpt_buffer_device_address(None, 1) == 0
+    assert wcpt.lib.wcpt_destroy(None) == 0
+    n = C.c_int(-1)
+    assert wcpt.lib.wcpt_device_count(C.byref(n)) == 0 and n.value >= 0
+
+
+def test_python_package_fails_loudly_without_library(tmp_path):
+    """No silent fallback: importing the package with the .so missing raises."""
+    import shutil
+    import subprocess
+    import sys
+    pkg = tmp_path / "pkg"
+    shutil.copytree(os.path.join(ROOT, "wc-path-tracer_amd", "wcpt"), pkg / "wcpt")
+    r = subprocess.run([sys.executable, "-c", "import wcpt"], cwd=pkg, capture_output=True, text=True)
+    assert r.returncode != 0 and "libwcpt.so not found" in r.stderr

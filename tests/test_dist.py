@@ -1,0 +1,69 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): row-block partition + gather reproduce the single-rank
+frame bit for bit. The per-rank renderer here is the CPU oracle; on GPUs bench.py runs the
+same partition with libwcpt.so per rank and the gather over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from wcpt.dist import gather_frame, row_block
+
+
+def test_row_block_partition():
+    for H in (1, 7, 135, 1080, 2160, 1081):
+        for N in (1, 2, 3, 4, 8):
+            if N > H:
+                continue
+            blocks = [row_block(H, N, r) for r in range(N)]
+            assert blocks[0][0] == 0
+            assert sum(r for _, r in blocks) == H
+            for (a, ra), (b, _) in zip(blocks, blocks[1:]):
+                assert a + ra == b
+            assert max(r for _, r in blocks) - min(r for _, r in blocks) <= 1
+    assert row_block(1080, 8, 7) == (945, 135)
+    with pytest.raises(ValueError):
+        row_block(10, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, out_path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "wc-path-tracer_amd"), os.path.join(root, "oracle")]
+    import oracle
+    from wcpt import scene as wscene
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = wscene.generate("cornell")
+    y0, rows = row_block(H, world, rank)
+    img, _ = oracle.render_scene(s, W, H, max_bounce=4, frame=3, y0=y0, rows=rows)
+    shard = torch.zeros((-(-H // world), W, 4), dtype=torch.float32)
+    shard[:rows] = torch.from_numpy(img)
+    frame = gather_frame(shard, H, world, rank)
+    if rank == 0:
+        np.save(out_path, frame.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_reassembles_frame(tmp_path, world):
+    import oracle
+    from wcpt import scene as wscene
+    W, H = 48, 37
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_worker, args=(world, _free_port(), W, H, out), nprocs=world, join=True)
+    full, _ = oracle.render_scene(wscene.generate("cornell"), W, H, max_bounce=4, frame=3)
+    assert np.array_equal(np.load(out), full)
