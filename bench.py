@@ -185,7 +185,7 @@ def main():
             "data": "synthetic (procedural scene generated in-process, no dataset)",
             "config": {"workload": desc, "config": args.config, "scene": name, "width": W, "height": H,
                        "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
-                       "kernel": ["megakernel", "persistent", "wavefront"][args.kernel],
+                       "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel],
                        "parallelism": f"row-block x{world}" + (" + RCCL gather" if world > 1 else "")},
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
             "segments_per_frame": int(segs_all / args.steps),

@@ -56,8 +56,11 @@ extern "C" {
 
 /* ---- kernel variants ---------------------------------------------------------------------------- */
 #define WCPT_KERNEL_MEGAKERNEL  0  /* one lane per pixel, exact reference semantics (default)          */
-#define WCPT_KERNEL_PERSISTENT  1  /* persistent waves, lanes refill with new pixels (same semantics)  */
 #define WCPT_KERNEL_WAVEFRONT   2  /* split ray-gen / traverse / shade queues (same semantics)         */
+
+/* ---- tuning options (wcpt_set_option); none changes results ------------------------------------- */
+#define WCPT_OPTION_STACK       1  /* traversal stack: 0 = scratch, 1 = LDS + scratch spill (default)   */
+#define WCPT_OPTION_DIAGNOSTICS 2  /* 1: wcpt_render_counters also fills the SIMD-efficiency fields      */
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 
@@ -141,6 +144,12 @@ typedef struct wcpt_counters {
     uint64_t triangle_tests;  /* rayTriangleIntersect calls (:170)                                 */
     uint64_t hits;            /* segments that hit (material fetched, :251)                        */
     uint64_t draw_fetches;    /* DrawCommand fetches (:153)                                        */
+    /* SIMD-efficiency diagnostics of this implementation (not reference work; 0 from the oracle):
+     * per phase, wave-steps (a wave executed the step with >= 1 lane) and lane-steps (lanes that did).
+     * lane/(64*wave) is the fraction of the 64 lanes doing useful work in that phase. */
+    uint64_t wave_interior_steps, lane_interior_steps;
+    uint64_t wave_triangle_steps, lane_triangle_steps;
+    uint64_t wave_segment_steps, lane_segment_steps;
 } wcpt_counters;
 
 /* Host mesh produced by the OBJ loader (ModelLoader.jai:60-141) or a scene generator. Memory is owned
@@ -173,6 +182,7 @@ int         wcpt_destroy(wcpt_context* ctx);                       /* Deinit, Pa
 const char* wcpt_last_error(const wcpt_context* ctx);              /* ctx may be NULL: last global error */
 int         wcpt_set_stream(wcpt_context* ctx, void* hip_stream);  /* NULL: the context's own stream     */
 int         wcpt_set_kernel(wcpt_context* ctx, int variant);       /* WCPT_KERNEL_*                       */
+int         wcpt_set_option(wcpt_context* ctx, int option, int value); /* WCPT_OPTION_*                   */
 
 /* ---- device buffers (BufferManager.jai) ------------------------------------------------------------ */
 int      wcpt_buffer_alloc(wcpt_context* ctx, uint64_t bytes, wcpt_buffer* out);

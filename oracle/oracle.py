@@ -20,7 +20,8 @@ COUNTER_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_v
 
 
 class _Counters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS]
+    # wcpt_counters of include/wcpt.h: the 8 reference counters + 6 implementation diagnostics (left 0 here)
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [(f"_diag{i}", C.c_uint64) for i in range(6)]
 
 
 class _Draw(C.Structure):

@@ -43,8 +43,9 @@ def assert_close(img, ref, exact=True):
         assert same == 1.0, f"bit-exact fraction {same:.6f}"
 
 
-def gpu_render(ctx, s, W, H, bounces=3, spp=1, frame=0, y0=0, rows=None, init=None, sd=None):
+def gpu_render(ctx, s, W, H, bounces=3, spp=1, frame=0, y0=0, rows=None, init=None, sd=None, kernel=None):
     dev = wcpt.DeviceScene(ctx, s)
+    ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL if kernel is None else kernel)
     try:
         ctx.create_screen(W, H)
         ctx.set_row_range(y0, rows or 0)
@@ -58,8 +59,12 @@ def gpu_render(ctx, s, W, H, bounces=3, spp=1, frame=0, y0=0, rows=None, init=No
         cnt = ctx.render_counters(sd, *dev.addresses())
     finally:
         ctx.set_row_range(0, 0)
+        ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
         dev.free()
     return img, cnt
+
+
+KERNELS = [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT]
 
 
 # ---- device functions -----------------------------------------------------------------------------------
@@ -116,44 +121,65 @@ def test_device_random_direction(gpu_ctx):
     ("cornell", 67, 45, 4, 3),          # ragged: not a multiple of the 8x8 tile
     ("atrium", 96, 54, 4, 1),
 ])
-def test_frame_parity(gpu_ctx, name, W, H, bounces, spp):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_frame_parity(gpu_ctx, name, W, H, bounces, spp, kernel):
     s = get_scene(name)
-    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp)
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, kernel=kernel)
     ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, threads=8)
     assert_close(img, ref)
     assert cnt == rcnt
 
 
-def test_progressive_accumulation(gpu_ctx):
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("stack", [0, 1])
+def test_stack_kinds_match_oracle(gpu_ctx, stack, kernel):
+    """Every traversal-stack implementation (scratch, LDS + spill) gives the oracle's image and counters."""
+    s = get_scene("atrium")
+    gpu_ctx.set_option(wcpt._lib.OPTION_STACK, stack)
+    init = np.full((64, 120, 4), 0.5, np.float32)
+    try:
+        img, cnt = gpu_render(gpu_ctx, s, 120, 64, bounces=4, frame=1, init=init, kernel=kernel)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_STACK, 1)
+    ref, rcnt = oracle.render_scene(s, 120, 64, max_bounce=4, frame=1, image=init, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_progressive_accumulation(gpu_ctx, kernel):
     """renderedFramesCount > 0 mixes into the existing image (pathTracer.comp:314-318)."""
     s = get_scene("default_dielectric")
     W, H = 48, 40
     rng = np.random.default_rng(3)
     init = rng.uniform(0, 1, (H, W, 4)).astype(np.float32)
     for frame in (1, 7, 1000):
-        img, _ = gpu_render(gpu_ctx, s, W, H, bounces=3, frame=frame, init=init)
+        img, _ = gpu_render(gpu_ctx, s, W, H, bounces=3, frame=frame, init=init, kernel=kernel)
         ref, _ = oracle.render_scene(s, W, H, max_bounce=3, frame=frame, image=init)
         assert_close(img, ref)
 
 
-def test_row_block_shards_equal_full_frame(gpu_ctx):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_row_block_shards_equal_full_frame(gpu_ctx, kernel):
     """the union of row blocks is bit-identical to the full-frame render."""
     s = get_scene("cornell")
     W, H = 80, 72
-    full, _ = gpu_render(gpu_ctx, s, W, H, bounces=4)
+    full, _ = gpu_render(gpu_ctx, s, W, H, bounces=4, kernel=kernel)
     parts = []
     for r in range(3):
         y0, rows = row_block(H, 3, r)
-        img, _ = gpu_render(gpu_ctx, s, W, H, bounces=4, y0=y0, rows=rows)
+        img, _ = gpu_render(gpu_ctx, s, W, H, bounces=4, y0=y0, rows=rows, kernel=kernel)
         parts.append(img)
     assert np.array_equal(np.concatenate(parts), full)
 
 
-def test_full_size_rows_vs_oracle(gpu_ctx):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_full_size_rows_vs_oracle(gpu_ctx, kernel):
     """BASELINE config 2 at full size (1920x1080, 4 bounces): oracle on sampled row bands of the same frame."""
     s = get_scene("cornell")
     W, H = 1920, 1080
-    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=5)
+    init = np.zeros((H, W, 4), np.float32)
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=5, init=init, kernel=kernel)
     assert cnt["pixels"] == W * H
     assert cnt["segments"] <= W * H * 5
     for y0 in (0, 333, 540, 1072):

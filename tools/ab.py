@@ -1,0 +1,66 @@
+"""A/B kernel variants in one process (interleaved, n rounds) on a bench config.
+
+    python tools/ab.py --config c3 --variants "stack=0" "stack=1" [--frames 5 --rounds 3]
+
+Each variant string is a comma list of option=value (stack=<0|1>, kernel=<0|1|2>). Prints per-variant
+median kernel ms/frame (HIP events on the context stream) and Mray/s.
+"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "wc-path-tracer_amd"), ROOT]
+
+import wcpt  # noqa: E402
+from wcpt import scene as wscene  # noqa: E402
+import bench  # noqa: E402  (CONFIGS)
+
+
+def apply(ctx, spec):
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        if k == "stack":
+            ctx.set_option(wcpt._lib.OPTION_STACK, int(v))
+        elif k == "kernel":
+            ctx.set_kernel(int(v))
+        else:
+            raise SystemExit(f"unknown option {k}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--variants", nargs="+", default=["stack=1"])
+    ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
+    s = wscene.generate(name)
+    ctx = wcpt.Context(0)
+    dev = wcpt.DeviceScene(ctx, s)
+    ctx.create_screen(W, H)
+    sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
+    segs = sum(ctx.render_counters(sd, *dev.addresses())["segments"] for sd in sds)
+    res = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for v in a.variants:
+            apply(ctx, v)
+            ctx.profile_begin()
+            for sd in sds:
+                ctx.render(sd, *dev.addresses())
+            ms, n = ctx.profile_end()
+            ctx.sync()
+            if r > 0:
+                res[v].append(ms / n)
+    print(f"{a.config}: {desc}; {segs / a.frames:.0f} segments/frame")
+    for v, t in res.items():
+        m = statistics.median(t)
+        print(f"  {v:30s} {m:8.3f} ms/frame  {segs / a.frames / m / 1e3:9.1f} Mray/s   (runs {', '.join(f'{x:.3f}' for x in t)})")
+    dev.free()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

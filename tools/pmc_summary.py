@@ -1,0 +1,64 @@
+"""Aggregate rocprofv3 --pmc CSVs (tools/pmc.sh) per kernel: mean counter value per dispatch.
+
+    python tools/pmc_summary.py gpurun_out/<tag>/pmc [--kernel pt_megakernel<false] [--json out.json]
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads half the bytes of wide
+coalesced reads on gfx950, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes; our reads are 16-byte
+per-lane gathers, an access width the guide leaves uncalibrated (stated wherever the number is used).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(d):
+    per = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            name = row.get("Kernel_Name", "")
+            per[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", default="pt_megakernel<false")
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--config", default=None)
+    ap.add_argument("--kernel-id", type=int, default=0)
+    a = ap.parse_args()
+    per = load(a.dir)
+    out = {}
+    for name, ctrs in per.items():
+        if a.kernel not in name:
+            continue
+        for c, vals in ctrs.items():
+            out[c] = sum(vals) / len(vals)
+    if not out:
+        raise SystemExit(f"no dispatches of {a.kernel} in {a.dir}")
+    d = dict(out)
+    if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
+        d["hbm_bytes_per_launch"] = int((2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024)
+    if "SQ_ACTIVE_INST_VALU" in out and "SQ_THREAD_CYCLES_VALU" in out and out["SQ_ACTIVE_INST_VALU"]:
+        d["valu_lane_utilization"] = out["SQ_THREAD_CYCLES_VALU"] / (64.0 * out["SQ_ACTIVE_INST_VALU"])
+    if "SQ_WAVE_CYCLES" in out and out["SQ_WAVE_CYCLES"]:
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in out:
+                d[k + "_frac"] = out[k] / out["SQ_WAVE_CYCLES"]
+    if "TCC_HIT_sum" in out and "TCC_MISS_sum" in out:
+        d["l2_hit_rate"] = out["TCC_HIT_sum"] / max(1.0, out["TCC_HIT_sum"] + out["TCC_MISS_sum"])
+    if a.config:
+        d["config"] = a.config
+        d["kernel"] = a.kernel_id
+    d["kernel_name_filter"] = a.kernel
+    print(json.dumps(d, indent=1))
+    if a.json:
+        json.dump(d, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -159,19 +159,88 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c)
 /* Per-lane work counters; reduced per wave and added to global u64 counters. */
 struct Counters {
     uint32_t pixels, segments, sphere_tests, node_pops, interior_visits, triangle_tests, hits, draw_fetches;
+    uint32_t wave_int, lane_int, wave_tri, lane_tri, wave_seg, lane_seg; /* SIMD-efficiency diagnostics */
 };
 
-/* Traversal stack in private (scratch) memory; entries = (node index, box entry t0). */
+/* Diagnostic step counting (COUNT kernels only): every executing lane adds a lane-step, the lowest active
+ * lane adds the wave-step. */
+template <bool DIAG>
+__device__ __forceinline__ void simd_step(uint32_t& wave, uint32_t& lane_steps)
+{
+    if (!DIAG) return;
+    const unsigned long long m = __ballot(1);
+    lane_steps++;
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) wave++;
+}
+
+/* Traversal stacks; entries = (node index, box entry distance t0) of deferred far children.
+ *
+ * PrivateStack keeps the entries in private (scratch) memory: simple, but every push/pop is a VMEM store/load
+ * that the per-XCD L2 cannot hold at full occupancy (measured: ~6 GB of writes per 1080p atrium frame).
+ * LdsStack keeps the first N entries in LDS, lane-interleaved ([entry][64 lanes] of 8-byte words: one
+ * conflict-free ds_write_b64 / ds_read_b64 per wave), and only entries N..N+SPILL-1 in scratch. */
 template <int N>
 struct PrivateStack {
     uint32_t idx[N];
     float t0[N];
+    int sp;
+    __device__ __forceinline__ void reset() { sp = 0; }
+    __device__ __forceinline__ bool empty() const { return sp == 0; }
+    __device__ __forceinline__ bool push(uint32_t i, float t)
+    {
+        if (sp >= N) return false;
+        idx[sp] = i;
+        t0[sp] = t;
+        sp++;
+        return true;
+    }
+    __device__ __forceinline__ void pop(uint32_t& i, float& t)
+    {
+        sp--;
+        i = idx[sp];
+        t = t0[sp];
+    }
+};
+
+template <int N, int SPILL>
+struct LdsStack {
+    uint2* base; /* &lds[0][lane] */
+    uint32_t sidx[SPILL];
+    float st0[SPILL];
+    int sp;
+    __device__ __forceinline__ void reset() { sp = 0; }
+    __device__ __forceinline__ bool empty() const { return sp == 0; }
+    __device__ __forceinline__ bool push(uint32_t i, float t)
+    {
+        if (sp < N) {
+            base[sp * 64] = make_uint2(i, __float_as_uint(t));
+        } else if (sp < N + SPILL) {
+            sidx[sp - N] = i;
+            st0[sp - N] = t;
+        } else {
+            return false;
+        }
+        sp++;
+        return true;
+    }
+    __device__ __forceinline__ void pop(uint32_t& i, float& t)
+    {
+        sp--;
+        if (sp < N) {
+            const uint2 e = base[sp * 64];
+            i = e.x;
+            t = __uint_as_float(e.y);
+        } else {
+            i = sidx[sp - N];
+            t = st0[sp - N];
+        }
+    }
 };
 
 /* pathTracer.comp:135-211 */
-template <bool COUNT, int STACK>
+template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
-                                         const wcpt_draw_command* __restrict__ draws, PrivateStack<STACK>& stk,
+                                         const wcpt_draw_command* __restrict__ draws, Stack& stk,
                                          Counters& cnt, bool& overflow)
 {
     Hit rec;
@@ -181,7 +250,10 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     rec.material = 0;
     rec.p = mk3(0.0f, 0.0f, 0.0f);
     rec.normal = mk3(0.0f, 0.0f, 0.0f);
-    if (COUNT) cnt.segments++;
+    if (COUNT) {
+        cnt.segments++;
+        simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
+    }
 
     for (uint32_t i = 0; i < sd.sphereCount; i++) {
         const wcpt_sphere& s = spheres[i];
@@ -209,7 +281,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         node_box(ray, cur, c0, c1);
         if (c0 > c1 || c1 < 0.0f || c0 > rec.t) continue;
         uint32_t curLeft = cur.b.z, curCount = cur.b.w;
-        int sp = 0;
+        stk.reset();
         for (;;) {
             if (curCount > 0) {
                 /* leaf (:164-178) */
@@ -222,7 +294,10 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                     const f3 b = ld3(vertices + 3ull * ib);
                     const f3 c = ld3(vertices + 3ull * ic);
                     const float t = rayTriangle(ray, a, b, c);
-                    if (COUNT) cnt.triangle_tests++;
+                    if (COUNT) {
+                        cnt.triangle_tests++;
+                        simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
+                    }
                     if (t != -1.0f && t < rec.t) {
                         rec.t = t;
                         rec.normal = normalize(cross(b - a, c - a));
@@ -237,7 +312,11 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 float l0, l1, r0, r1;
                 node_box(ray, L, l0, l1);
                 node_box(ray, R, r0, r1);
-                if (COUNT) { cnt.interior_visits++; cnt.node_pops += 2; }
+                if (COUNT) {
+                    cnt.interior_visits++;
+                    cnt.node_pops += 2;
+                    simd_step<DIAG>(cnt.wave_int, cnt.lane_int);
+                }
                 const float leftDist = (l0 > 0.0f) ? l0 : l1;
                 const float rightDist = (r0 > 0.0f) ? r0 : r1;
                 const bool passL = !(l0 > l1 || l1 < 0.0f);
@@ -249,15 +328,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 const bool passFar = leftFirst ? passR : passL;
                 const float nearT0 = leftFirst ? l0 : r0;
                 const float farT0 = leftFirst ? r0 : l0;
-                if (passFar) {
-                    if (sp < STACK) {
-                        stk.idx[sp] = farIdx;
-                        stk.t0[sp] = farT0;
-                        sp++;
-                    } else {
-                        overflow = true;
-                    }
-                }
+                if (passFar && !stk.push(farIdx, farT0)) overflow = true;
                 if (passNear && !(nearT0 > rec.t)) {
                     const NodeV& N = leftFirst ? L : R;
                     curLeft = N.b.z;
@@ -267,10 +338,10 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
             }
             /* pop (:157-162) */
             bool found = false;
-            while (sp > 0) {
-                sp--;
-                const uint32_t ni = stk.idx[sp];
-                const float t0 = stk.t0[sp];
+            while (!stk.empty()) {
+                uint32_t ni;
+                float t0;
+                stk.pop(ni, t0);
                 if (t0 > rec.t) continue;
                 const uint2 lc = reinterpret_cast<const uint2*>(bvh + ni)[3];
                 curLeft = lc.x;
@@ -317,53 +388,88 @@ __device__ __forceinline__ f3 ray_color(const Ray& r)
     return mk3(0.5f * ia + 1.0f * a, 0.7f * ia + 1.0f * a, 1.0f * ia + 1.0f * a);
 }
 
+/* State of one path between segments: the loop-carried variables of TraceRay (pathTracer.comp:241-245). */
+struct PathState {
+    Ray ray;
+    f3 totalLight;
+    f3 transmittance;
+    uint32_t bounce; /* loop index i of :245 */
+};
+
+__device__ __forceinline__ void path_begin(PathState& ps, f3 origin, f3 dir)
+{
+    ps.ray.origin = origin;
+    ps.ray.direction = dir;
+    ps.ray.invDirection = rcp3(dir);
+    ps.totalLight = mk3(0.0f, 0.0f, 0.0f);
+    ps.transmittance = mk3(1.0f, 1.0f, 1.0f);
+    ps.bounce = 0;
+}
+
+/* Shading after an Intersect (pathTracer.comp:248-280). Returns true when the path is finished, with its
+ * radiance in L: on a miss (:248-249) or when the bounce loop is exhausted (:245, :283). */
+__device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t& rng, const wcpt_scene_data& sd,
+                                           const wcpt_material* __restrict__ mats, f3& L)
+{
+    Ray& ray = ps.ray;
+    if (!h.hit) {
+        L = ps.totalLight + ray_color(ray) * ps.transmittance;
+        return true;
+    }
+    const wcpt_material& m = mats[h.material];
+    const uint32_t mtype = m.type;
+    const f3 emission = ld3(m.emission);
+    const float emissionStrength = m.emissionStrength;
+    const float roughness = m.roughness;
+    ps.totalLight = ps.totalLight + (emission * emissionStrength) * ps.transmittance;
+
+    if (mtype == WCPT_MATERIAL_METAL) {
+        ray.origin = h.p + h.normal * kBias;
+        const f3 R = reflect(ray.direction, h.normal);
+        const f3 rd = RandomDirection(rng);
+        ray.direction = normalize(R + roughness * rd);
+        ray.invDirection = rcp3(ray.direction);
+        ps.transmittance = ps.transmittance * ld3(m.albedo);
+    } else {
+        const float ior = m.ior;
+        const float etaI = h.front ? 1.0f : ior;
+        const float etaT = h.front ? ior : 1.0f;
+        const float reflectProb = CalculateReflectance(ray.direction, h.normal, etaI, etaT);
+        const f3 R = reflect(ray.direction, h.normal);
+        const f3 T = refract(ray.direction, h.normal, etaI / etaT);
+        bool followReflection = (T.x == 0.0f && T.y == 0.0f && T.z == 0.0f);
+        if (!followReflection) followReflection = (rand_f(rng) <= reflectProb); /* :273 short-circuit */
+        const f3 rd = RandomDirection(rng);
+        ray.direction = normalize((followReflection ? R : T) + roughness * rd);
+        ray.invDirection = rcp3(ray.direction);
+        if (!followReflection && !h.front) {
+            const f3 e = ((ld3(m.absorption) * -1.0f) * m.absorptionStrength) * h.t;
+            ps.transmittance = ps.transmittance * mk3(wcpt_expf(e.x), wcpt_expf(e.y), wcpt_expf(e.z));
+        }
+        ray.origin = h.p + (kBias * h.normal) * sign1(dot(ray.direction, h.normal));
+    }
+    ps.bounce++;
+    if (ps.bounce > sd.maxBounceCount) { /* loop exhausted: no sky term (:283) */
+        L = ps.totalLight;
+        return true;
+    }
+    return false;
+}
+
 /* pathTracer.comp:241-284 */
-template <bool COUNT, int STACK>
+template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_data& sd,
                                        const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
-                                       const wcpt_draw_command* __restrict__ draws, PrivateStack<STACK>& stk,
+                                       const wcpt_draw_command* __restrict__ draws, Stack& stk,
                                        Counters& cnt, bool& overflow)
 {
-    f3 totalLight = mk3(0.0f, 0.0f, 0.0f);
-    f3 transmittance = mk3(1.0f, 1.0f, 1.0f);
-    for (uint32_t i = 0; i <= sd.maxBounceCount; i++) {
-        const Hit h = intersect<COUNT, STACK>(ray, sd, spheres, draws, stk, cnt, overflow);
-        if (!h.hit) return totalLight + ray_color(ray) * transmittance;
-
-        const wcpt_material& m = mats[h.material];
-        const uint32_t mtype = m.type;
-        const f3 emission = ld3(m.emission);
-        const float emissionStrength = m.emissionStrength;
-        const float roughness = m.roughness;
-        totalLight = totalLight + (emission * emissionStrength) * transmittance;
-
-        if (mtype == WCPT_MATERIAL_METAL) {
-            ray.origin = h.p + h.normal * kBias;
-            const f3 R = reflect(ray.direction, h.normal);
-            const f3 rd = RandomDirection(rng);
-            ray.direction = normalize(R + roughness * rd);
-            ray.invDirection = rcp3(ray.direction);
-            transmittance = transmittance * ld3(m.albedo);
-        } else {
-            const float ior = m.ior;
-            const float etaI = h.front ? 1.0f : ior;
-            const float etaT = h.front ? ior : 1.0f;
-            const float reflectProb = CalculateReflectance(ray.direction, h.normal, etaI, etaT);
-            const f3 R = reflect(ray.direction, h.normal);
-            const f3 T = refract(ray.direction, h.normal, etaI / etaT);
-            bool followReflection = (T.x == 0.0f && T.y == 0.0f && T.z == 0.0f);
-            if (!followReflection) followReflection = (rand_f(rng) <= reflectProb); /* :273 short-circuit */
-            const f3 rd = RandomDirection(rng);
-            ray.direction = normalize((followReflection ? R : T) + roughness * rd);
-            ray.invDirection = rcp3(ray.direction);
-            if (!followReflection && !h.front) {
-                const f3 e = ((ld3(m.absorption) * -1.0f) * m.absorptionStrength) * h.t;
-                transmittance = transmittance * mk3(wcpt_expf(e.x), wcpt_expf(e.y), wcpt_expf(e.z));
-            }
-            ray.origin = h.p + (kBias * h.normal) * sign1(dot(ray.direction, h.normal));
-        }
+    PathState ps;
+    path_begin(ps, ray.origin, ray.direction);
+    f3 L;
+    for (;;) {
+        const Hit h = intersect<COUNT, DIAG>(ps.ray, sd, spheres, draws, stk, cnt, overflow);
+        if (path_shade(ps, h, rng, sd, mats, L)) return L;
     }
-    return totalLight;
 }
 
 /* pathTracer.comp:290-302 — primary ray direction for pixel (x, y) of a W x H frame. */
@@ -395,6 +501,29 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
+}
+
+/* Wave-reduce the per-lane counters into the 14 global u64 counters (wcpt_counters order). All 64 lanes of
+ * the wave must call it. */
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const Counters& cnt, unsigned long long* __restrict__ counters)
+{
+    if (COUNT) {
+        wave_add_u64(&counters[0], cnt.pixels);
+        wave_add_u64(&counters[1], cnt.segments);
+        wave_add_u64(&counters[2], cnt.sphere_tests);
+        wave_add_u64(&counters[3], cnt.node_pops);
+        wave_add_u64(&counters[4], cnt.interior_visits);
+        wave_add_u64(&counters[5], cnt.triangle_tests);
+        wave_add_u64(&counters[6], cnt.hits);
+        wave_add_u64(&counters[7], cnt.draw_fetches);
+        wave_add_u64(&counters[8], cnt.wave_int);
+        wave_add_u64(&counters[9], cnt.lane_int);
+        wave_add_u64(&counters[10], cnt.wave_tri);
+        wave_add_u64(&counters[11], cnt.lane_tri);
+        wave_add_u64(&counters[12], cnt.wave_seg);
+        wave_add_u64(&counters[13], cnt.lane_seg);
+    }
 }
 
 } // namespace dev

@@ -10,9 +10,12 @@
 namespace wcpt {
 
 /* Traversal stack entries per lane. The reference declares 32 (pathTracer.comp:151), which a depth-32
- * midpoint BVH can overflow; our far-child stack needs at most tree depth entries. Deeper trees set the
- * WCPT_ERROR_STACK_OVERFLOW status instead of writing out of bounds. */
-constexpr int kStackDepth = 48;
+ * midpoint BVH can overflow; our far-child stack needs at most (tree depth - 1) entries. Deeper trees set
+ * the WCPT_ERROR_STACK_OVERFLOW status instead of writing out of bounds. */
+constexpr int kPrivateStack = 48;          /* stack kind 0: all entries in scratch                         */
+constexpr int kLdsStack = 16;              /* stack kind 1: entries in LDS (16 x 8 B x 64 lanes = 8 KiB/wave) */
+constexpr int kSpillStack = 32;            /*               + entries 16..47 spilled to scratch              */
+constexpr int kStackDepth = kLdsStack + kSpillStack;
 
 struct LaunchArgs {
     wcpt_scene_data sd;
@@ -25,7 +28,38 @@ struct LaunchArgs {
     unsigned long long* counters;
 };
 
-hipError_t launch_megakernel(const LaunchArgs& a, bool count, hipStream_t stream);
+/* Wavefront path state (pt_wavefront.hip): structure-of-arrays in one device allocation. */
+struct WfBuffers {
+    float4* ray0;      /* (origin.xyz, direction.x)                       */
+    float4* ray1;      /* (direction.yz, bounce bits, sample bits)        */
+    float4* light;     /* (totalLight.xyz, rng state bits)                */
+    float4* trans;     /* (transmittance.xyz, -)                          */
+    float4* result;    /* (sum of sample radiance .xyz, -)                */
+    float4* hit;       /* (t, normal.xyz) of the last Intersect            */
+    uint2* hitinfo;    /* (material, flags)                               */
+    uint32_t* queue_in;
+    uint32_t* count_in;
+    uint32_t* queue_out;
+    uint32_t* count_out;
+    uint32_t* head;    /* trace kernel's dequeue position                 */
+};
+struct WfState {
+    void* mem = nullptr;
+    uint32_t capacity = 0;
+    float4 *ray0 = nullptr, *ray1 = nullptr, *light = nullptr, *trans = nullptr, *result = nullptr, *hit = nullptr;
+    uint2* hitinfo = nullptr;
+    uint32_t* queue[2] = {nullptr, nullptr};
+    uint32_t* ctr = nullptr;
+};
+
+/* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD
+ * diagnostics (ballot-based step counters, tools/diag.py). */
+constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
+
+hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream);
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, hipStream_t stream);
+hipError_t wf_reserve(WfState& s, uint32_t paths);
+void wf_release(WfState& s);
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n,
                            hipStream_t stream);
 

@@ -4,6 +4,10 @@
  * Launch shape: one 64-lane wave per 8x8 pixel tile (the reference's 4x4 = 16-invocation workgroups would
  * leave 48 of 64 lanes idle on wave64 CDNA). A bounds guard makes any width/height legal (the reference
  * has none, :289). SceneData arrives by value in the kernarg segment.
+ *
+ * Instantiations: COUNT=false renders; COUNT=true runs the same frame without writing the image and counts the
+ * reference algorithm's work; DIAG=true additionally counts SIMD lane/wave steps with a
+ * __ballot inside the traversal loop (tools/diag.py only — kept out of the COUNT build the parity tests use).
  */
 #include <hip/hip_runtime.h>
 
@@ -19,15 +23,53 @@ namespace dev {
 __device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTotal, uint32_t& tx, uint32_t& ty)
 {
     const uint32_t b = blockIdx.x;
-    const uint32_t per = (tilesTotal + 7u) / 8u;
-    const uint32_t xcd = b & 7u, k = b >> 3;
-    uint32_t t = xcd * per + k;
-    if (t >= tilesTotal || (tilesTotal & 7u) != 0u) t = b; /* exact band split only when divisible by 8 */
+    uint32_t t = b;
+    if ((tilesTotal & 7u) == 0u) t = (b & 7u) * (tilesTotal >> 3) + (b >> 3);
     tx = t % tilesX;
     ty = t / tilesX;
 }
 
-template <bool COUNT, int STACK>
+/* Shade one pixel (pathTracer.comp:290-323) with the given traversal stack. */
+template <bool COUNT, bool DIAG, class Stack>
+__device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcpt_material* __restrict__ mats,
+                                            const wcpt_sphere* __restrict__ spheres,
+                                            const wcpt_draw_command* __restrict__ draws, float4* __restrict__ image,
+                                            uint32_t W, uint32_t H, uint32_t y0, uint32_t lx, uint32_t ly, Stack& stk,
+                                            Counters& cnt, bool& overflow)
+{
+    const uint32_t x = lx, y = y0 + ly;
+    const f3 dir = primary_direction(sd, x, y, W, H);
+    const uint32_t pixel_index = x + y * W + sd.renderedFramesCount * 719393u; /* :304 */
+    uint32_t seed = pcg_hash(pixel_index);
+    f3 result = mk3(0.0f, 0.0f, 0.0f);
+    const f3 origin = mk3(sd.position[0], sd.position[1], sd.position[2]);
+    for (uint32_t s = 0; s < sd.samples; s++) { /* :309-310, all samples share the primary ray */
+        Ray r;
+        r.origin = origin;
+        r.direction = dir;
+        r.invDirection = rcp3(dir);
+        result = result + TraceRay<COUNT, DIAG>(r, seed, sd, mats, spheres, draws, stk, cnt, overflow);
+    }
+    result = result / (float)sd.samples; /* :312 */
+    if (!COUNT) {
+        float4* px = image + (size_t)ly * W + lx;
+        f3 acc;
+        if (sd.renderedFramesCount == 0) { /* :318 — the loaded value would be discarded */
+            acc = result;
+        } else {
+            const float4 o = *px;                                             /* :314 */
+            const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u); /* :316 */
+            const float iw = 1.0f - weight;
+            acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight, o.z * iw + result.z * weight);
+        }
+        *px = make_float4(acc.x, acc.y, acc.z, 1.0f); /* :323 */
+    }
+    if (COUNT) cnt.pixels++;
+}
+
+/* Stack kinds: 0 = private (scratch) stack of kPrivateStack entries; 1 = LDS stack of kLdsStack entries per
+ * lane with a kSpillStack-entry private spill. */
+template <bool COUNT, bool DIAG, int SK>
 __global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                     const wcpt_sphere* __restrict__ spheres,
                                                     const wcpt_draw_command* __restrict__ draws,
@@ -40,51 +82,21 @@ __global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, co
     tile_of_block(tilesX, tilesTotal, tx, ty);
     const uint32_t lx = tx * 8u + (threadIdx.x & 7u);
     const uint32_t ly = ty * 8u + (threadIdx.x >> 3);
-    const bool active = lx < W && ly < rows;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cnt = {};
     bool overflow = false;
-    if (active) {
-        const uint32_t x = lx, y = y0 + ly;
-        const f3 dir = primary_direction(sd, x, y, W, H);
-        const uint32_t pixel_index = x + y * W + sd.renderedFramesCount * 719393u; /* :304 */
-        uint32_t seed = pcg_hash(pixel_index);
-        PrivateStack<STACK> stk;
-        f3 result = mk3(0.0f, 0.0f, 0.0f);
-        const f3 origin = mk3(sd.position[0], sd.position[1], sd.position[2]);
-        for (uint32_t s = 0; s < sd.samples; s++) { /* :309-310, all samples share the primary ray */
-            Ray r;
-            r.origin = origin;
-            r.direction = dir;
-            r.invDirection = rcp3(dir);
-            result = result + TraceRay<COUNT, STACK>(r, seed, sd, mats, spheres, draws, stk, cnt, overflow);
+    if (lx < W && ly < rows) {
+        if constexpr (SK == 0) {
+            PrivateStack<kPrivateStack> stk;
+            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, image, W, H, y0, lx, ly, stk, cnt, overflow);
+        } else {
+            __shared__ uint2 s_stack[kLdsStack * 64];
+            LdsStack<kLdsStack, kSpillStack> stk;
+            stk.base = s_stack + (threadIdx.x & 63u);
+            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, image, W, H, y0, lx, ly, stk, cnt, overflow);
         }
-        result = result / (float)sd.samples; /* :312 */
-        if (!COUNT) {
-            float4* px = image + (size_t)ly * W + lx;
-            f3 acc;
-            if (sd.renderedFramesCount == 0) { /* :318 — the loaded value would be discarded */
-                acc = result;
-            } else {
-                const float4 o = *px;                                          /* :314 */
-                const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u); /* :316 */
-                const float iw = 1.0f - weight;
-                acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight, o.z * iw + result.z * weight);
-            }
-            *px = make_float4(acc.x, acc.y, acc.z, 1.0f);                     /* :323 */
-        }
-        if (COUNT) cnt.pixels = 1;
     }
     if (overflow) atomicOr(status, 1u);
-    if (COUNT) {
-        wave_add_u64(&counters[0], cnt.pixels);
-        wave_add_u64(&counters[1], cnt.segments);
-        wave_add_u64(&counters[2], cnt.sphere_tests);
-        wave_add_u64(&counters[3], cnt.node_pops);
-        wave_add_u64(&counters[4], cnt.interior_visits);
-        wave_add_u64(&counters[5], cnt.triangle_tests);
-        wave_add_u64(&counters[6], cnt.hits);
-        wave_add_u64(&counters[7], cnt.draw_fetches);
-    }
+    flush_counters<COUNT>(cnt, counters);
 }
 
 /* Device self-tests: evaluate the device definitions of the RNG and the deterministic libm on host inputs. */
@@ -121,19 +133,28 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
 } // namespace dev
 
 /* ------------------------------------------------------------------------------------------------ */
-hipError_t launch_megakernel(const LaunchArgs& a, bool count, hipStream_t stream)
+template <bool COUNT, bool DIAG, int SK>
+static void launch_mega(const LaunchArgs& a, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
+{
+    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK>), dim3(tiles), dim3(64), 0, stream, a.sd, a.materials,
+                       a.spheres, a.draws, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
+}
+
+hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tilesY = (a.rows + 7u) / 8u;
     const uint32_t tiles = tilesX * tilesY;
     if (tiles == 0) return hipSuccess;
-    const dim3 grid(tiles), block(64);
-    if (count)
-        hipLaunchKernelGGL((dev::pt_megakernel<true, kStackDepth>), grid, block, 0, stream, a.sd, a.materials, a.spheres,
-                           a.draws, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
-    else
-        hipLaunchKernelGGL((dev::pt_megakernel<false, kStackDepth>), grid, block, 0, stream, a.sd, a.materials, a.spheres,
-                           a.draws, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
+    if (stack_kind == 0) {
+        if (mode == kModeRender) launch_mega<false, false, 0>(a, stream, tilesX, tiles);
+        else if (mode == kModeCount) launch_mega<true, false, 0>(a, stream, tilesX, tiles);
+        else launch_mega<true, true, 0>(a, stream, tilesX, tiles);
+    } else {
+        if (mode == kModeRender) launch_mega<false, false, 1>(a, stream, tilesX, tiles);
+        else if (mode == kModeCount) launch_mega<true, false, 1>(a, stream, tilesX, tiles);
+        else launch_mega<true, true, 1>(a, stream, tilesX, tiles);
+    }
     return hipGetLastError();
 }
 

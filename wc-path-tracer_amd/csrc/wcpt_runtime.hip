@@ -21,6 +21,7 @@
 
 namespace {
 
+constexpr int kNumCounters = 14; /* wcpt_counters: 8 reference counters + 6 diagnostics */
 std::mutex g_err_mutex;
 std::string g_last_error;
 
@@ -45,9 +46,12 @@ struct wcpt_context {
     bool sharded = false;
     uint32_t* d_status = nullptr;
     unsigned long long* d_counters = nullptr;
+    wcpt::WfState wf;                  /* path state of the wavefront kernels (allocated on first use) */
     uint32_t* d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
+    int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + scratch spill */
+    int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
     std::string last_error;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -129,7 +133,7 @@ int alloc_image(wcpt_context* ctx, uint32_t w, uint32_t h, uint32_t y0, uint32_t
 }
 
 int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
-                  uint64_t draws, bool count)
+                  uint64_t draws, int mode)
 {
     int rc = bind(ctx);
     if (rc) return rc;
@@ -155,7 +159,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.status = ctx->d_status;
     a.counters = ctx->d_counters;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (ctx->profiling && !count) {
+    if (ctx->profiling && mode == wcpt::kModeRender) {
         if (ctx->events_used == ctx->events.size()) {
             hipEvent_t b, c;
             HIP_TRY(ctx, hipEventCreate(&b), "hipEventCreate");
@@ -169,7 +173,8 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     }
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
-    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, count, ctx->stream); break;
+    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->stream); break;
+    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->stream); break;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
@@ -236,7 +241,7 @@ int wcpt_create(int device, wcpt_context** out_ctx)
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_status, 4);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_counters, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_counters, kNumCounters * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 4);
     if (e != hipSuccess) {
         int rc = hip_fail(nullptr, e, "wcpt_create");
@@ -258,6 +263,7 @@ int wcpt_destroy(wcpt_context* ctx)
     if (ctx->own_image) (void)hipFree(ctx->own_image);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    wcpt::wf_release(ctx->wf);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     for (auto& p : ctx->events) {
         (void)hipEventDestroy(p.first);
@@ -280,10 +286,25 @@ int wcpt_set_stream(wcpt_context* ctx, void* hip_stream)
 int wcpt_set_kernel(wcpt_context* ctx, int variant)
 {
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
-    if (variant != WCPT_KERNEL_MEGAKERNEL)
+    if (variant != WCPT_KERNEL_MEGAKERNEL && variant != WCPT_KERNEL_WAVEFRONT)
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", variant);
     ctx->kernel = variant;
     return WCPT_SUCCESS;
+}
+
+int wcpt_set_option(wcpt_context* ctx, int option, int value)
+{
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    switch (option) {
+    case WCPT_OPTION_DIAGNOSTICS:
+        ctx->diagnostics = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_STACK:
+        if (value < 0 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "stack kind %d", value);
+        ctx->stack_kind = value;
+        return WCPT_SUCCESS;
+    default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown option %d", option);
+    }
 }
 
 /* ---- buffers ------------------------------------------------------------------------------------ */
@@ -473,7 +494,7 @@ int wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes)
 int wcpt_render(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                 uint64_t draw_commands)
 {
-    return render_common(ctx, scene, materials, spheres, draw_commands, false);
+    return render_common(ctx, scene, materials, spheres, draw_commands, wcpt::kModeRender);
 }
 
 int wcpt_sync(wcpt_context* ctx)
@@ -490,10 +511,11 @@ int wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64
     int rc = bind(ctx);
     if (rc) return rc;
     if (!out) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null counters");
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), ctx->stream), "hipMemsetAsync");
-    rc = render_common(ctx, scene, materials, spheres, draw_commands, true);
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream), "hipMemsetAsync");
+    rc = render_common(ctx, scene, materials, spheres, draw_commands,
+                       ctx->diagnostics ? wcpt::kModeDiag : wcpt::kModeCount);
     if (rc) return rc;
-    unsigned long long h[8];
+    unsigned long long h[kNumCounters];
     HIP_TRY(ctx, hipMemcpyAsync(h, ctx->d_counters, sizeof(h), hipMemcpyDeviceToHost, ctx->stream), "hipMemcpyAsync");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     out->pixels = h[0];
@@ -504,6 +526,12 @@ int wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64
     out->triangle_tests = h[5];
     out->hits = h[6];
     out->draw_fetches = h[7];
+    out->wave_interior_steps = h[8];
+    out->lane_interior_steps = h[9];
+    out->wave_triangle_steps = h[10];
+    out->lane_triangle_steps = h[11];
+    out->wave_segment_steps = h[12];
+    out->lane_segment_steps = h[13];
     return read_status(ctx);
 }
 

@@ -3,14 +3,14 @@
 The compute lives in libwcpt.so (hand-written HIP for gfx950 behind the C-ABI of include/wcpt.h); this
 package is the Python host mirror used by tests and the benchmark.
 """
-from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL, KERNEL_PERSISTENT,
+from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL,
                    KERNEL_WAVEFRONT, LIB_PATH, MATERIAL_DIELECTRIC, MATERIAL_DTYPE, MATERIAL_METAL, NODE_DTYPE,
                    SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, WcptError, lib)
 from .renderer import Context, DeviceScene, PathTracingRenderer
 from . import scene
 
 __all__ = [
-    "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL", "KERNEL_PERSISTENT",
+    "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
     "PathTracingRenderer", "scene", "device_count",

@@ -36,8 +36,10 @@ MATERIAL_METAL = 0
 MATERIAL_DIELECTRIC = 1
 
 KERNEL_MEGAKERNEL = 0
-KERNEL_PERSISTENT = 1
 KERNEL_WAVEFRONT = 2
+
+OPTION_STACK = 1
+OPTION_DIAGNOSTICS = 2
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
@@ -55,15 +57,18 @@ DRAW_COMMAND_DTYPE = np.dtype([("vertexBuffer", "<u8"), ("indexBuffer", "<u8"), 
                                ("indexCount", "<u4"), ("_pad", "<u4")])
 COUNTER_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",
                   "hits", "draw_fetches")
+DIAG_FIELDS = ("wave_interior_steps", "lane_interior_steps", "wave_triangle_steps", "lane_triangle_steps",
+               "wave_segment_steps", "lane_segment_steps")
 assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
 assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
 
 
 class Counters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS + DIAG_FIELDS]
 
-    def as_dict(self):
-        return {n: int(getattr(self, n)) for n in COUNTER_FIELDS}
+    def as_dict(self, diagnostics: bool = False):
+        names = COUNTER_FIELDS + (DIAG_FIELDS if diagnostics else ())
+        return {n: int(getattr(self, n)) for n in names}
 
 
 class Mesh(C.Structure):
@@ -97,6 +102,7 @@ _PROTOTYPES = {
     "wcpt_last_error": (C.c_char_p, [_p]),
     "wcpt_set_stream": (_i, [_p, _p]),
     "wcpt_set_kernel": (_i, [_p, _i]),
+    "wcpt_set_option": (_i, [_p, _i, _i]),
     "wcpt_buffer_alloc": (_i, [_p, _u64, C.POINTER(_u64)]),
     "wcpt_buffer_upload": (_i, [_p, _u64, _p, _u64, _u64]),
     "wcpt_buffer_download": (_i, [_p, _u64, _p, _u64, _u64]),

@@ -11,7 +11,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, MATERIAL_DTYPE, SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera,
+from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, OPTION_DIAGNOSTICS, MATERIAL_DTYPE, SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera,
                    Counters, WcptError, check, lib, ptr)
 from . import scene as _scene
 
@@ -49,6 +49,9 @@ class Context:
     # -- configuration -------------------------------------------------------------------------------
     def set_kernel(self, variant: int):
         self._chk(lib.wcpt_set_kernel(self.h, variant))
+
+    def set_option(self, option: int, value: int):
+        self._chk(lib.wcpt_set_option(self.h, option, value))
 
     def set_stream(self, stream_handle: int | None):
         self._chk(lib.wcpt_set_stream(self.h, stream_handle or None))
@@ -125,11 +128,18 @@ class Context:
     def sync(self):
         self._chk(lib.wcpt_sync(self.h))
 
-    def render_counters(self, sd: np.ndarray, materials: int, spheres: int, draws: int) -> dict:
+    def render_counters(self, sd: np.ndarray, materials: int, spheres: int, draws: int,
+                        diagnostics: bool = False) -> dict:
+        """Reference-algorithm work counters of one frame (COUNTER_FIELDS); with diagnostics=True also the
+        implementation's SIMD-efficiency step counters (DIAG_FIELDS)."""
         sd = np.ascontiguousarray(sd, dtype=SCENE_DATA_DTYPE)
         c = Counters()
-        self._chk(lib.wcpt_render_counters(self.h, ptr(sd), materials, spheres, draws, C.byref(c)))
-        return c.as_dict()
+        self._chk(lib.wcpt_set_option(self.h, OPTION_DIAGNOSTICS, 1 if diagnostics else 0))
+        try:
+            self._chk(lib.wcpt_render_counters(self.h, ptr(sd), materials, spheres, draws, C.byref(c)))
+        finally:
+            lib.wcpt_set_option(self.h, OPTION_DIAGNOSTICS, 0)
+        return c.as_dict(diagnostics)
 
     def profile_begin(self):
         self._chk(lib.wcpt_profile_begin(self.h))
