@@ -61,6 +61,7 @@ extern "C" {
 /* ---- tuning options (wcpt_set_option); none changes results ------------------------------------- */
 #define WCPT_OPTION_STACK       1  /* traversal stack: 0 = scratch, 1 = LDS + scratch spill (default)   */
 #define WCPT_OPTION_DIAGNOSTICS 2  /* 1: wcpt_render_counters also fills the SIMD-efficiency fields      */
+#define WCPT_OPTION_SORT_RAYS   3  /* wavefront: sort bounce rays by (octant, origin Morton) (default 0) */
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 
@@ -218,6 +219,10 @@ int      wcpt_sync(wcpt_context* ctx);
  * Does not write the image. Synchronous. */
 int      wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials,
                               uint64_t spheres, uint64_t draw_commands, wcpt_counters* out);
+
+/* Wavefront trace-loop phase timers of the last wcpt_render_counters call with WCPT_OPTION_DIAGNOSTICS set
+ * (s_memtime cycles summed over waves): {fetch, leaf, interior, pop, epilogue, waves, iterations, -}. */
+int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
 
 /* ---- kernel timing (HIP events on the context's stream) -------------------------------------------- */
 int      wcpt_profile_begin(wcpt_context* ctx);

@@ -1,9 +1,10 @@
 """A/B kernel variants in one process (interleaved, n rounds) on a bench config.
 
-    python tools/ab.py --config c3 --variants "stack=0" "stack=1" [--frames 5 --rounds 3]
+    python tools/ab.py --config c3 --variants "kernel=0" "kernel=2" "kernel=2,deindex=1" [--frames 5 --rounds 3]
 
-Each variant string is a comma list of option=value (stack=<0|1>, kernel=<0|1|2>). Prints per-variant
-median kernel ms/frame (HIP events on the context stream) and Mray/s.
+Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, deindex=<0|1> (mesh re-laid out in
+BVH leaf order with identity indices: same triangles, same results, soup-like locality). Prints the median
+ms/frame (HIP events on the context stream) and Mray/s.
 """
 import argparse
 import os
@@ -13,40 +14,50 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "wc-path-tracer_amd"), ROOT]
 
+import numpy as np  # noqa: E402
 import wcpt  # noqa: E402
 from wcpt import scene as wscene  # noqa: E402
 import bench  # noqa: E402  (CONFIGS)
 
 
-def apply(ctx, spec):
-    for kv in filter(None, spec.split(",")):
-        k, v = kv.split("=")
-        if k == "stack":
-            ctx.set_option(wcpt._lib.OPTION_STACK, int(v))
-        elif k == "kernel":
-            ctx.set_kernel(int(v))
-        else:
-            raise SystemExit(f"unknown option {k}")
+def parse(spec):
+    return dict(kv.split("=") for kv in filter(None, spec.split(",")))
+
+
+def deindexed(s):
+    import copy
+    d = copy.copy(s)
+    d.meshes = []
+    for m in s.meshes:
+        pos = np.ascontiguousarray(m.positions[m.indices])
+        d.meshes.append(wscene.HostBVH(pos, np.arange(m.indices.size, dtype=np.uint32), m.nodes))
+    return d
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--variants", nargs="+", default=["stack=1"])
+    ap.add_argument("--variants", nargs="+", default=["kernel=0"])
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
     ctx = wcpt.Context(0)
-    dev = wcpt.DeviceScene(ctx, s)
+    scenes = {"0": wcpt.DeviceScene(ctx, s)}
+    if any(parse(v).get("deindex") == "1" for v in a.variants):
+        scenes["1"] = wcpt.DeviceScene(ctx, deindexed(s))
     ctx.create_screen(W, H)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
-    segs = sum(ctx.render_counters(sd, *dev.addresses())["segments"] for sd in sds)
+    segs = sum(ctx.render_counters(sd, *scenes["0"].addresses())["segments"] for sd in sds)
     res = {v: [] for v in a.variants}
     for r in range(a.rounds + 1):
         for v in a.variants:
-            apply(ctx, v)
+            o = parse(v)
+            ctx.set_option(wcpt._lib.OPTION_STACK, int(o.get("stack", 1)))
+            ctx.set_kernel(int(o.get("kernel", 0)))
+            ctx.set_option(wcpt._lib.OPTION_SORT_RAYS, int(o.get("sort", 0)))
+            dev = scenes[o.get("deindex", "0")]
             ctx.profile_begin()
             for sd in sds:
                 ctx.render(sd, *dev.addresses())
@@ -58,7 +69,8 @@ def main():
     for v, t in res.items():
         m = statistics.median(t)
         print(f"  {v:30s} {m:8.3f} ms/frame  {segs / a.frames / m / 1e3:9.1f} Mray/s   (runs {', '.join(f'{x:.3f}' for x in t)})")
-    dev.free()
+    for d in scenes.values():
+        d.free()
     ctx.close()
 
 

@@ -1,6 +1,6 @@
-"""SIMD-efficiency diagnostics of the instrumented kernel: per phase, useful lanes / (64 * wave-steps).
+"""SIMD-efficiency and trace-loop phase diagnostics of the instrumented (DIAG) kernels.
 
-    python tools/diag.py --config c3 [--kernel 0]
+    python tools/diag.py --config c3 [--kernel 0|2] [--size WxH] [--stack 0|1]
 """
 import argparse
 import json
@@ -39,6 +39,15 @@ def main():
         out[f"simd_eff_{ph}"] = round(l / (64.0 * w), 4) if w else None
     out["per_segment"] = {k: round(c[k] / c["segments"], 3) for k in ("interior_visits", "triangle_tests",
                                                                        "node_pops", "sphere_tests")}
+    if a.kernel == 2:
+        t = ctx.read_diagnostics()
+        tot = sum(t[:5]) or 1
+        out["trace_phase_share"] = {k: round(v / tot, 4) for k, v in
+                                    zip(("fetch", "leaf", "interior", "pop", "epilogue"), t[:5])}
+        out["trace_waves"], out["trace_iterations"] = t[5], t[6]
+        if t[6]:
+            out["trace_cycles_per_iteration"] = round(tot / t[6], 1)
+            out["trace_iterations_per_wave"] = round(t[6] / max(1, t[5]), 1)
     print(a.config, "kernel", a.kernel, json.dumps(out, indent=1))
     dev.free()
     ctx.close()

@@ -25,6 +25,18 @@
 namespace wcpt {
 namespace dev {
 
+/* Scene buffers are reached through device addresses stored in DrawCommands (buffer device addresses in the
+ * reference, pathTracer.comp:82-88). Casting them to address-space-1 (global) pointers makes hipcc emit
+ * global_load_* instead of flat_load_*: flat loads count against lgkmcnt as well as vmcnt, so every LDS
+ * stack access would otherwise also wait for outstanding node fetches. */
+#define WCPT_GLOBAL __attribute__((address_space(1)))
+typedef const WCPT_GLOBAL wcpt_node* gnode_ptr;
+typedef const WCPT_GLOBAL uint32_t* gu32_ptr;
+typedef const WCPT_GLOBAL float* gf32_ptr;
+__device__ __forceinline__ gnode_ptr as_nodes(uint64_t a) { return (gnode_ptr)(uintptr_t)a; }
+__device__ __forceinline__ gu32_ptr as_u32(uint64_t a) { return (gu32_ptr)(uintptr_t)a; }
+__device__ __forceinline__ gf32_ptr as_f32(uint64_t a) { return (gf32_ptr)(uintptr_t)a; }
+
 /* constants.glsl:4-9 */
 constexpr float kBias = 1e-5f;
 constexpr float kInfinity = 3.402823466e+38f;
@@ -58,6 +70,10 @@ __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)
 }
 __device__ __forceinline__ float sign1(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 __device__ __forceinline__ f3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+__device__ __forceinline__ f3 ld3(gf32_ptr p) { return mk3(p[0], p[1], p[2]); } /* global_load_dwordx3 */
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 /* ---- Random.glsl:10-56 ------------------------------------------------------------------------- */
 __device__ __forceinline__ uint32_t pcg_hash(uint32_t seed)
@@ -115,14 +131,20 @@ __device__ __forceinline__ void rayBox(const Ray& r, float mnx_, float mny_, flo
 }
 
 /* A BVH node (32 B) as two 16-byte loads: {min.xyz, max.x}, {max.yz, left, count}. */
-struct NodeV { float4 a; uint4 b; };
-__device__ __forceinline__ NodeV load_node(const wcpt_node* __restrict__ bvh, uint32_t i)
+struct NodeV { v4f a; v4u b; };
+__device__ __forceinline__ NodeV load_node(gnode_ptr bvh, uint32_t i)
 {
-    const float4* p = reinterpret_cast<const float4*>(bvh + i);
+    const WCPT_GLOBAL v4f* p = reinterpret_cast<const WCPT_GLOBAL v4f*>(bvh + i);
     NodeV n;
     n.a = p[0];
-    n.b = reinterpret_cast<const uint4*>(p)[1];
+    n.b = reinterpret_cast<const WCPT_GLOBAL v4u*>(p)[1];
     return n;
+}
+/* (leftNodeOrTriangleIndex, triangleCount) of node i: bytes 24..31 */
+__device__ __forceinline__ uint2 load_node_lc(gnode_ptr bvh, uint32_t i)
+{
+    const v2u v = reinterpret_cast<const WCPT_GLOBAL v2u*>(bvh + i)[3];
+    return make_uint2(v.x, v.y);
 }
 __device__ __forceinline__ void node_box(const Ray& r, const NodeV& n, float& t0, float& t1)
 {
@@ -270,9 +292,9 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     }
 
     for (uint32_t i = 0; i < sd.drawCommandCount; i++) {
-        const wcpt_node* __restrict__ bvh = reinterpret_cast<const wcpt_node*>(draws[i].bvhBuffer);
-        const uint32_t* __restrict__ indices = reinterpret_cast<const uint32_t*>(draws[i].indexBuffer);
-        const float* __restrict__ vertices = reinterpret_cast<const float*>(draws[i].vertexBuffer);
+        const gnode_ptr bvh = as_nodes(draws[i].bvhBuffer);
+        const gu32_ptr indices = as_u32(draws[i].indexBuffer);
+        const gf32_ptr vertices = as_f32(draws[i].vertexBuffer);
         if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
 
         /* root: pushed untested, popped and tested (:155-162) */
@@ -343,7 +365,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 float t0;
                 stk.pop(ni, t0);
                 if (t0 > rec.t) continue;
-                const uint2 lc = reinterpret_cast<const uint2*>(bvh + ni)[3];
+                const uint2 lc = load_node_lc(bvh, ni);
                 curLeft = lc.x;
                 curCount = lc.y;
                 found = true;

@@ -42,6 +42,7 @@ struct WfBuffers {
     uint32_t* queue_out;
     uint32_t* count_out;
     uint32_t* head;    /* trace kernel's dequeue position                 */
+    unsigned long long* diag; /* DIAG builds: trace-loop phase timers (8 x u64) */
 };
 struct WfState {
     void* mem = nullptr;
@@ -50,6 +51,11 @@ struct WfState {
     uint2* hitinfo = nullptr;
     uint32_t* queue[2] = {nullptr, nullptr};
     uint32_t* ctr = nullptr;
+    unsigned long long* diag = nullptr;
+    void* sort_mem = nullptr;
+    uint32_t *sort_keys = nullptr, *sort_keys_alt = nullptr, *sort_vals = nullptr;
+    void* sort_temp = nullptr;
+    size_t sort_temp_bytes = 0;
 };
 
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD
@@ -57,7 +63,8 @@ struct WfState {
 constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream);
-hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, hipStream_t stream);
+/* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, hipStream_t stream);
 hipError_t wf_reserve(WfState& s, uint32_t paths);
 void wf_release(WfState& s);
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n,

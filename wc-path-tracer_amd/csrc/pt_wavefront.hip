@@ -21,6 +21,7 @@
  * changes. Path state lives in HBM as structure-of-arrays float4s (80 B/path + 24 B hit record).
  */
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "pt_device.h"
 #include "pt_kernels.h"
@@ -110,60 +111,95 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
 }
 
 /* ---- trace ------------------------------------------------------------------------------------------ */
+/* Register budget: the trace loop carries only the ray (9), the closest hit as (t, primitive id) (2-3), a
+ * 3-word node cursor and the stack pointer; the normal and material of the winning primitive are rebuilt
+ * once per ray in the epilogue with the reference's expressions (:145, :173), which gives bit-identical
+ * values. With the 10-entry LDS stack (5 KiB/wave) and __launch_bounds__(64, 8) the kernel runs 8 waves per
+ * SIMD (32 per CU) to keep more dependent node fetches in flight. */
+constexpr int kWfLdsStack = 10;
+constexpr int kWfSpill = kStackDepth - kWfLdsStack;
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
+constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
-struct Trav {
-    const wcpt_node* bvh;
-    const uint32_t* indices;
-    const float* vertices;
-    uint32_t d, curLeft, curCount, k, mode;
+struct Geom {
+    gnode_ptr bvh;
+    gu32_ptr indices;
+    gf32_ptr vertices;
 };
 
-/* Start draw command t.d (or the next one whose root survives the cull, :152-162); kModeDone past the last. */
-template <bool COUNT, class Stack>
-__device__ __forceinline__ void start_draw(Trav& t, const Ray& ray, float recT, const wcpt_scene_data& sd,
-                                           const wcpt_draw_command* __restrict__ draws, Stack& stk, Counters& cnt)
+__device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ draws, uint32_t d)
 {
-    for (; t.d < sd.drawCommandCount; t.d++) {
-        t.bvh = reinterpret_cast<const wcpt_node*>(draws[t.d].bvhBuffer);
-        t.indices = reinterpret_cast<const uint32_t*>(draws[t.d].indexBuffer);
-        t.vertices = reinterpret_cast<const float*>(draws[t.d].vertexBuffer);
-        if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
-        const NodeV root = load_node(t.bvh, 0);
-        float c0, c1;
-        node_box(ray, root, c0, c1);
-        if (c0 > c1 || c1 < 0.0f || c0 > recT) continue;
-        t.curLeft = root.b.z;
-        t.curCount = root.b.w;
-        t.k = 0;
-        t.mode = t.curCount > 0 ? kModeLeaf : kModeInterior;
-        stk.reset();
-        return;
-    }
-    t.mode = kModeDone;
+    Geom g;
+    g.bvh = as_nodes(draws[d].bvhBuffer);
+    g.indices = as_u32(draws[d].indexBuffer);
+    g.vertices = as_f32(draws[d].vertexBuffer);
+    return g;
 }
 
-template <bool COUNT, bool DIAG>
-__global__ __launch_bounds__(64) void wf_trace(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
-                                               const wcpt_draw_command* __restrict__ draws, WfBuffers b,
-                                               uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
+/* DIAG builds only: per-wave cycle timers (s_memtime) of the trace loop's phases, summed over waves into
+ * b.diag[0..4] = {fetch+loop, leaf, interior, pop, epilogue}, [5] = waves, [6] = loop iterations. The stamps
+ * add their own cost; read the shares, not the totals (cdna_hip_programming.md §7, In-kernel stamps). */
+constexpr int kDiagTimers = 8;
+template <bool DIAG>
+__device__ __forceinline__ void diag_mark(uint64_t* tim, uint64_t& tprev, int k)
 {
-    __shared__ uint2 s_stack[kLdsStack * 64];
+    if (!DIAG) return;
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    tim[k] += t - tprev;
+    tprev = t;
+    if (k == 0) tim[6] += 1;
+}
+
+/* Node cursor: interior -> (a = left child index); leaf -> (a = current index position, b = end position). */
+__device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, uint32_t& a, uint32_t& b, uint32_t& mode)
+{
+    a = left;
+    b = left + count;
+    mode = count > 0 ? kModeLeaf : kModeInterior;
+}
+
+template <bool COUNT, bool DIAG, bool SINGLE>
+__global__ __launch_bounds__(64, 8) void wf_trace(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
+                                                  const wcpt_draw_command* __restrict__ draws, WfBuffers b,
+                                                  uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
+{
+    __shared__ uint2 s_stack[kWfLdsStack * 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.count_out = 0; /* shade appends to it after this kernel */
     const uint32_t n = *b.count_in;
     const uint32_t lane = lane_id();
-    LdsStack<kLdsStack, kSpillStack> stk;
+    LdsStack<kWfLdsStack, kWfSpill> stk;
     stk.base = s_stack + lane;
     Counters cnt = {};
     bool overflow = false;
+    Geom g0 = {nullptr, nullptr, nullptr}, gl = {nullptr, nullptr, nullptr};
+    if (SINGLE) g0 = load_geom(draws, 0); /* kernel-uniform: scalar registers */
 
     bool has = false, drained = false;
     uint32_t lo = 0, hi = 0; /* this wave's claimed queue range [lo, hi) (wave-uniform) */
-    uint32_t p = 0;
+    uint32_t p = 0, d = 0, prim = kNoPrim, primDraw = 0;
+    uint32_t ca = 0, cb = 0, mode = kModeDone;
+    float rt = kInfinity;
     Ray ray;
-    Hit rec;
-    Trav t;
-    t.mode = kModeDone;
+    uint64_t tim[kDiagTimers] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = DIAG ? __builtin_amdgcn_s_memtime() : 0;
+
+    /* Start draw command d, or the next one whose root survives the cull (:152-162); kModeDone past the last. */
+    auto start_draw = [&]() {
+        for (; d < sd.drawCommandCount; d++) {
+            if (!SINGLE) gl = load_geom(draws, d);
+            const Geom& g = SINGLE ? g0 : gl;
+            if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
+            const NodeV root = load_node(g.bvh, 0);
+            float c0, c1;
+            node_box(ray, root, c0, c1);
+            if (c0 > c1 || c1 < 0.0f || c0 > rt) continue;
+            cursor_from(root.b.z, root.b.w, ca, cb, mode);
+            stk.reset();
+            return;
+        }
+        mode = kModeDone;
+    };
+
     for (;;) {
         /* dynamic fetch: idle lanes take the next queued rays */
         if (!drained) {
@@ -190,30 +226,23 @@ __global__ __launch_bounds__(64) void wf_trace(const wcpt_scene_data sd, const w
                     ray.direction = mk3(r0.w, r1.x, r1.y);
                     ray.invDirection = rcp3(ray.direction);
                     /* Intersect prologue (:136-149): the sphere loop */
-                    rec.t = kInfinity;
-                    rec.hit = false;
-                    rec.front = false;
-                    rec.material = 0;
-                    rec.normal = mk3(0.0f, 0.0f, 0.0f);
+                    rt = kInfinity;
+                    prim = kNoPrim;
                     if (COUNT) {
                         cnt.segments++;
                         simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
                     }
                     for (uint32_t i = 0; i < sd.sphereCount; i++) {
                         const wcpt_sphere& s = spheres[i];
-                        const f3 spc = mk3(s.position[0], s.position[1], s.position[2]);
-                        const float tempRec = raySphereNear(ray, spc, s.radius);
+                        const float tempRec = raySphereNear(ray, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
                         if (COUNT) cnt.sphere_tests++;
-                        if (tempRec > 0.0f && tempRec < rec.t) {
-                            rec.t = tempRec;
-                            rec.p = ray.origin + rec.t * ray.direction;
-                            rec.normal = (rec.p - spc) / s.radius;
-                            rec.hit = true;
-                            rec.material = s.material;
+                        if (tempRec > 0.0f && tempRec < rt) {
+                            rt = tempRec;
+                            prim = kSpherePrim | i;
                         }
                     }
-                    t.d = 0;
-                    start_draw<COUNT>(t, ray, rec.t, sd, draws, stk, cnt);
+                    d = 0;
+                    start_draw();
                     has = true;
                 }
                 const uint32_t took = min(avail, (uint32_t)__popcll(need));
@@ -222,32 +251,33 @@ __global__ __launch_bounds__(64) void wf_trace(const wcpt_scene_data sd, const w
             }
         }
         if (!__ballot(has)) break;
-        if (has) {
-            /* one traversal step (:157-200) */
-            if (t.mode == kModeLeaf) {
-                const uint32_t first = t.k + t.curLeft;
-                const uint32_t ia = t.indices[first + 0];
-                const uint32_t ib = t.indices[first + 1];
-                const uint32_t ic = t.indices[first + 2];
-                const f3 a = ld3(t.vertices + 3ull * ia);
-                const f3 bb = ld3(t.vertices + 3ull * ib);
-                const f3 c = ld3(t.vertices + 3ull * ic);
-                const float tt = rayTriangle(ray, a, bb, c);
+        diag_mark<DIAG>(tim, tprev, 0);
+        {
+            const Geom& g = SINGLE ? g0 : gl;
+            /* one traversal step (:157-200); the phases are sequential ifs (a lane's mode changes only
+             * LEAF->POP or INTERIOR->{LEAF,INTERIOR,POP} in a step, so this equals if / else if) */
+            if (has && mode == kModeLeaf) {
+                const uint32_t ia = g.indices[ca + 0];
+                const uint32_t ib = g.indices[ca + 1];
+                const uint32_t ic = g.indices[ca + 2];
+                const float tt = rayTriangle(ray, ld3(g.vertices + 3ull * ia), ld3(g.vertices + 3ull * ib),
+                                             ld3(g.vertices + 3ull * ic));
                 if (COUNT) {
                     cnt.triangle_tests++;
                     simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
                 }
-                if (tt != -1.0f && tt < rec.t) {
-                    rec.t = tt;
-                    rec.normal = normalize(cross(bb - a, c - a));
-                    rec.hit = true;
-                    rec.material = 0; /* :175 */
+                if (tt != -1.0f && tt < rt) {
+                    rt = tt;
+                    prim = ca;
+                    primDraw = d;
                 }
-                t.k += 3;
-                if (t.k >= t.curCount) t.mode = kModePop;
-            } else if (t.mode == kModeInterior) {
-                const NodeV L = load_node(t.bvh, t.curLeft);
-                const NodeV R = load_node(t.bvh, t.curLeft + 1);
+                ca += 3;
+                if (ca >= cb) mode = kModePop;
+            }
+            diag_mark<DIAG>(tim, tprev, 1);
+            if (has && mode == kModeInterior) {
+                const NodeV L = load_node(g.bvh, ca);
+                const NodeV R = load_node(g.bvh, ca + 1);
                 float l0, l1, r0, r1;
                 node_box(ray, L, l0, l1);
                 node_box(ray, R, r0, r1);
@@ -261,59 +291,72 @@ __global__ __launch_bounds__(64) void wf_trace(const wcpt_scene_data sd, const w
                 const bool passL = !(l0 > l1 || l1 < 0.0f);
                 const bool passR = !(r0 > r1 || r1 < 0.0f);
                 const bool leftFirst = leftDist < rightDist;
-                const uint32_t farIdx = leftFirst ? t.curLeft + 1 : t.curLeft;
                 const bool passNear = leftFirst ? passL : passR;
                 const bool passFar = leftFirst ? passR : passL;
-                const float nearT0 = leftFirst ? l0 : r0;
-                const float farT0 = leftFirst ? r0 : l0;
-                if (passFar && !stk.push(farIdx, farT0)) overflow = true;
-                if (passNear && !(nearT0 > rec.t)) {
-                    const NodeV& N = leftFirst ? L : R;
-                    t.curLeft = N.b.z;
-                    t.curCount = N.b.w;
-                    t.k = 0;
-                    t.mode = t.curCount > 0 ? kModeLeaf : kModeInterior;
+                if (passFar && !stk.push(leftFirst ? ca + 1 : ca, leftFirst ? r0 : l0)) overflow = true;
+                if (passNear && !((leftFirst ? l0 : r0) > rt)) {
+                    const uint32_t nl = leftFirst ? L.b.z : R.b.z, nc = leftFirst ? L.b.w : R.b.w;
+                    cursor_from(nl, nc, ca, cb, mode);
                 } else {
-                    t.mode = kModePop;
+                    mode = kModePop;
                 }
             }
-            if (t.mode == kModePop) {
+            diag_mark<DIAG>(tim, tprev, 2);
+            if (has && mode == kModePop) {
                 bool found = false;
                 while (!stk.empty()) {
                     uint32_t ni;
                     float t0;
                     stk.pop(ni, t0);
-                    if (t0 > rec.t) continue;
-                    const uint2 lc = reinterpret_cast<const uint2*>(t.bvh + ni)[3];
-                    t.curLeft = lc.x;
-                    t.curCount = lc.y;
-                    t.k = 0;
-                    t.mode = t.curCount > 0 ? kModeLeaf : kModeInterior;
+                    if (t0 > rt) continue;
+                    const uint2 lc = load_node_lc(g.bvh, ni);
+                    cursor_from(lc.x, lc.y, ca, cb, mode);
                     found = true;
                     break;
                 }
                 if (!found) {
-                    t.d++;
-                    start_draw<COUNT>(t, ray, rec.t, sd, draws, stk, cnt);
+                    d++;
+                    start_draw();
                 }
             }
-            if (t.mode == kModeDone) {
-                /* Intersect epilogue (:204-208) */
-                uint32_t flags = 0;
-                if (rec.hit) {
-                    rec.front = dot(ray.direction, rec.normal) < 0.0f;
-                    if (!rec.front) rec.normal = rec.normal * -1.0f;
-                    flags = kHitFlag | (rec.front ? kFrontFlag : 0u);
+            diag_mark<DIAG>(tim, tprev, 3);
+            if (has && mode == kModeDone) {
+                /* Intersect epilogue (:204-208), with the winner's normal and material rebuilt as at :145/:173 */
+                uint32_t flags = 0, mat = 0;
+                f3 nrm = mk3(0.0f, 0.0f, 0.0f);
+                if (prim != kNoPrim) {
+                    if (prim & kSpherePrim) {
+                        const wcpt_sphere& s = spheres[prim & ~kSpherePrim];
+                        const f3 c = mk3(s.position[0], s.position[1], s.position[2]);
+                        const f3 ph = ray.origin + rt * ray.direction;
+                        nrm = (ph - c) / s.radius;
+                        mat = s.material;
+                    } else {
+                        const Geom gw = SINGLE ? g0 : load_geom(draws, primDraw);
+                        const f3 a = ld3(gw.vertices + 3ull * gw.indices[prim + 0]);
+                        const f3 bb = ld3(gw.vertices + 3ull * gw.indices[prim + 1]);
+                        const f3 c = ld3(gw.vertices + 3ull * gw.indices[prim + 2]);
+                        nrm = normalize(cross(bb - a, c - a));
+                        mat = 0; /* :175 */
+                    }
+                    const bool front = dot(ray.direction, nrm) < 0.0f;
+                    if (!front) nrm = nrm * -1.0f;
+                    flags = kHitFlag | (front ? kFrontFlag : 0u);
                     if (COUNT) cnt.hits++;
                 }
-                b.hit[p] = make_float4(rec.t, rec.normal.x, rec.normal.y, rec.normal.z);
-                b.hitinfo[p] = make_uint2(rec.material, flags);
+                b.hit[p] = make_float4(rt, nrm.x, nrm.y, nrm.z);
+                b.hitinfo[p] = make_uint2(mat, flags);
                 has = false;
             }
+            diag_mark<DIAG>(tim, tprev, 4);
         }
     }
     if (overflow) atomicOr(status, 1u);
     flush_counters<COUNT>(cnt, counters);
+    if (DIAG && lane == 0) {
+        tim[5] += 1; /* waves */
+        for (int k = 0; k < kDiagTimers; k++) atomicAdd(&b.diag[k], (unsigned long long)tim[k]);
+    }
 }
 
 /* ---- shade ------------------------------------------------------------------------------------------ */
@@ -416,7 +459,7 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     if (paths <= s.capacity) return hipSuccess;
     wf_release(s);
     const size_t P = paths;
-    const size_t bytes = P * (6 * sizeof(float4) + sizeof(uint2) + 2 * sizeof(uint32_t)) + 64;
+    const size_t bytes = P * (6 * sizeof(float4) + sizeof(uint2) + 2 * sizeof(uint32_t)) + 256;
     char* m = nullptr;
     hipError_t e = hipMalloc(&m, bytes);
     if (e != hipSuccess) return e;
@@ -432,27 +475,105 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     s.queue[0] = reinterpret_cast<uint32_t*>(s.hitinfo + P);
     s.queue[1] = s.queue[0] + P;
     s.ctr = s.queue[1] + P; /* [0] count q0, [1] count q1, [2] trace head */
+    s.diag = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(s.ctr + 4 + 7) & ~uintptr_t(7));
     s.capacity = paths;
+    /* ray-sort scratch: keys, alternate keys, sorted queue, radix-sort temporary storage */
+    size_t temp = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)paths, 0, 32);
+    if (e != hipSuccess) return e;
+    char* q = nullptr;
+    e = hipMalloc(&q, 3 * P * sizeof(uint32_t) + temp + 256);
+    if (e != hipSuccess) return e;
+    s.sort_mem = q;
+    s.sort_keys = reinterpret_cast<uint32_t*>(q);
+    s.sort_keys_alt = s.sort_keys + P;
+    s.sort_vals = s.sort_keys_alt + P;
+    s.sort_temp = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(s.sort_vals + P) + 255) & ~uintptr_t(255));
+    s.sort_temp_bytes = temp;
     return hipSuccess;
 }
 
 void wf_release(WfState& s)
 {
     if (s.mem) (void)hipFree(s.mem);
+    if (s.sort_mem) (void)hipFree(s.sort_mem);
     s = WfState{};
 }
 
-template <bool COUNT, bool DIAG>
+/* Ray sorting between bounces: key = direction octant (3 bits) | Morton code of the origin quantised to a
+ * 512^3 grid over the first draw's root box (27 bits); queue slots at or past the live count get the sentinel
+ * key 0xffffffff and sort to the end. Rays that start close together and head the same way then share a
+ * wave, so their node fetches hit the same cache lines (tools/gather_bench.hip: coherent gathers reach ~7x
+ * the scattered visit rate). The processing order of paths never affects their results. */
+__device__ __forceinline__ uint32_t spread3(uint32_t v)
+{
+    v &= 0x1FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void wf_sort_keys(WfBuffers b, uint32_t P, const wcpt_draw_command* __restrict__ draws,
+                                                    uint32_t* __restrict__ keys)
+{
+    const uint32_t n = *b.count_in;
+    const dev::gnode_ptr root = dev::as_nodes(draws[0].bvhBuffer);
+    const float lo[3] = {root->min[0], root->min[1], root->min[2]};
+    const float hi[3] = {root->max[0], root->max[1], root->max[2]};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n) {
+            const uint32_t p = b.queue_in[i];
+            const float4 r0 = b.ray0[p], r1 = b.ray1[p];
+            const float o[3] = {r0.x, r0.y, r0.z};
+            const uint32_t oct = (r0.w < 0.0f ? 4u : 0u) | (r1.x < 0.0f ? 2u : 0u) | (r1.y < 0.0f ? 1u : 0u);
+            uint32_t m = 0;
+            for (int a = 0; a < 3; a++) {
+                const float ext = hi[a] - lo[a];
+                float f = ext > 0.0f ? (o[a] - lo[a]) / ext : 0.0f;
+                f = fminf(fmaxf(f, 0.0f), 1.0f);
+                m |= spread3((uint32_t)(f * 511.0f)) << (2 - a);
+            }
+            key = (oct << 27) | m;
+        }
+        keys[i] = key;
+    }
+}
+
+template <bool COUNT, bool DIAG, bool SINGLE>
 static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace_grid, uint32_t shade_grid,
                          hipStream_t stream)
 {
-    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.spheres, a.draws, b,
-                       a.status, a.counters);
+    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.spheres,
+                       a.draws, b, a.status, a.counters);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials, b,
                        a.image, a.W, a.H, a.y0, a.counters);
 }
 
-hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, hipStream_t stream)
+template <bool COUNT, bool DIAG, bool SINGLE>
+static hipError_t trace_blocks_per_cu(int& bpc)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<COUNT, DIAG, SINGLE>, 64, 0);
+}
+
+static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b, uint32_t P, int cus,
+                             hipStream_t stream)
+{
+    const uint32_t grid = min((P + 255u) / 256u, (uint32_t)cus * 8u);
+    hipLaunchKernelGGL(wf_sort_keys, dim3(grid), dim3(256), 0, stream, b, P, a.draws, s.sort_keys);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t temp = s.sort_temp_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(s.sort_temp, temp, s.sort_keys, s.sort_keys_alt, b.queue_in, s.sort_vals,
+                                           (int)P, 0, 32, stream);
+    if (e != hipSuccess) return e;
+    return hipMemcpyAsync(b.queue_in, s.sort_vals, (size_t)P * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
+}
+
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, hipStream_t stream)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tilesY = (a.rows + 7u) / 8u;
@@ -467,12 +588,13 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, hipStream
     e = cu_count(cus);
     if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
-    static int trace_bpc[3] = {0, 0, 0};
-    int& bpc = trace_bpc[mode];
+    const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
+    static int trace_bpc[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    int& bpc = trace_bpc[mode][single ? 1 : 0];
     if (bpc == 0) {
-        if (mode == kModeRender) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<false, false>, 64, 0);
-        else if (mode == kModeCount) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<true, false>, 64, 0);
-        else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<true, true>, 64, 0);
+        if (mode == kModeRender) e = single ? trace_blocks_per_cu<false, false, true>(bpc) : trace_blocks_per_cu<false, false, false>(bpc);
+        else if (mode == kModeCount) e = single ? trace_blocks_per_cu<true, false, true>(bpc) : trace_blocks_per_cu<true, false, false>(bpc);
+        else e = single ? trace_blocks_per_cu<true, true, true>(bpc) : trace_blocks_per_cu<true, true, false>(bpc);
         if (e != hipSuccess) return e;
         if (bpc < 1) bpc = 1;
     }
@@ -483,7 +605,11 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, hipStream
     if (e != hipSuccess) return e;
     WfBuffers b;
     b.ray0 = s.ray0; b.ray1 = s.ray1; b.light = s.light; b.trans = s.trans; b.result = s.result;
-    b.hit = s.hit; b.hitinfo = s.hitinfo; b.head = s.ctr + 2;
+    b.hit = s.hit; b.hitinfo = s.hitinfo; b.head = s.ctr + 2; b.diag = s.diag;
+    if (mode == kModeDiag) {
+        e = hipMemsetAsync(s.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
     b.queue_in = s.queue[0]; b.count_in = s.ctr + 0;
     b.queue_out = s.queue[1]; b.count_out = s.ctr + 1;
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);
@@ -498,10 +624,21 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, hipStream
     /* each iteration advances every live path by one segment; a path needs <= samples*(maxBounce+1) */
     uint64_t iters = (uint64_t)a.sd.samples * ((uint64_t)a.sd.maxBounceCount + 1ull);
     if (iters > (1ull << 20)) iters = 1ull << 20; /* bounded; WCPT documents the cap */
+    sort_rays = sort_rays && a.sd.drawCommandCount > 0;
     for (uint64_t it = 0; it < iters; it++) {
-        if (mode == kModeRender) wf_iteration<false, false>(a, b, trace_grid, shade_grid, stream);
-        else if (mode == kModeCount) wf_iteration<true, false>(a, b, trace_grid, shade_grid, stream);
-        else wf_iteration<true, true>(a, b, trace_grid, shade_grid, stream);
+        if (sort_rays && it > 0) { /* bounce rays; the primary queue is already in 8x8-tile order */
+            e = sort_queue(a, s, b, P, cus, stream);
+            if (e != hipSuccess) return e;
+        }
+        if (single) {
+            if (mode == kModeRender) wf_iteration<false, false, true>(a, b, trace_grid, shade_grid, stream);
+            else if (mode == kModeCount) wf_iteration<true, false, true>(a, b, trace_grid, shade_grid, stream);
+            else wf_iteration<true, true, true>(a, b, trace_grid, shade_grid, stream);
+        } else {
+            if (mode == kModeRender) wf_iteration<false, false, false>(a, b, trace_grid, shade_grid, stream);
+            else if (mode == kModeCount) wf_iteration<true, false, false>(a, b, trace_grid, shade_grid, stream);
+            else wf_iteration<true, true, false>(a, b, trace_grid, shade_grid, stream);
+        }
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         std::swap(b.queue_in, b.queue_out);

@@ -25,10 +25,31 @@ constexpr int kNumCounters = 14; /* wcpt_counters: 8 reference counters + 6 diag
 std::mutex g_err_mutex;
 std::string g_last_error;
 
+/* Device buffers are handed out at base address = 32 (mod 64) (a 64-byte-aligned allocation + 32). A BVH
+ * node is 32 bytes and the two children of an interior node sit at indices (2k+1, 2k+2) (the builder appends
+ * them as a pair after the root, PathTracingRenderer.jai:196-202), so with this base every child pair the
+ * traversal fetches together occupies exactly one 64-byte cache line instead of straddling two. Scattered
+ * line visits are what bounds traversal (tools/gather_bench.hip). 32-byte alignment is enough for every
+ * other buffer type (largest access: 16 bytes). */
+constexpr uint64_t kBufferSkew = 32;
+
 struct Buffer {
-    void* ptr = nullptr;
+    void* raw = nullptr;   /* hipMalloc result */
+    void* ptr = nullptr;   /* raw + kBufferSkew: the device address handed out */
     uint64_t bytes = 0;
 };
+
+hipError_t skewed_alloc(Buffer& b, uint64_t bytes)
+{
+    b.raw = nullptr;
+    b.ptr = nullptr;
+    b.bytes = bytes;
+    if (!bytes) return hipSuccess;
+    hipError_t e = hipMalloc(&b.raw, bytes + 2 * kBufferSkew);
+    if (e != hipSuccess) return e;
+    b.ptr = static_cast<char*>(b.raw) + kBufferSkew;
+    return hipSuccess;
+}
 
 } // namespace
 
@@ -52,6 +73,7 @@ struct wcpt_context {
     int kernel = WCPT_KERNEL_MEGAKERNEL;
     int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + scratch spill */
     int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
+    int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
     std::string last_error;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -174,7 +196,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
     case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->stream); break;
-    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->stream); break;
+    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->sort_rays != 0, ctx->stream); break;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
@@ -259,7 +281,7 @@ int wcpt_destroy(wcpt_context* ctx)
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->buffers)
-        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+        if (kv.second.raw) (void)hipFree(kv.second.raw);
     if (ctx->own_image) (void)hipFree(ctx->own_image);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
@@ -296,6 +318,9 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
 {
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
     switch (option) {
+    case WCPT_OPTION_SORT_RAYS:
+        ctx->sort_rays = value ? 1 : 0;
+        return WCPT_SUCCESS;
     case WCPT_OPTION_DIAGNOSTICS:
         ctx->diagnostics = value ? 1 : 0;
         return WCPT_SUCCESS;
@@ -314,8 +339,7 @@ int wcpt_buffer_alloc(wcpt_context* ctx, uint64_t bytes, wcpt_buffer* out)
     if (rc) return rc;
     if (!out) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null out handle");
     Buffer b;
-    b.bytes = bytes;
-    if (bytes) HIP_TRY(ctx, hipMalloc(&b.ptr, bytes), "hipMalloc(buffer)");
+    HIP_TRY(ctx, skewed_alloc(b, bytes), "hipMalloc(buffer)");
     const uint64_t h = ctx->next_handle++;
     ctx->buffers[h] = b;
     *out = h;
@@ -331,19 +355,18 @@ int wcpt_buffer_upload(wcpt_context* ctx, wcpt_buffer buf, const void* src, uint
     if (bytes && !src) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null upload source");
     if (offset + bytes > b->bytes) {
         /* grow, keeping the old contents (BufferManager.jai:53-54 reallocates on growth) */
-        void* np = nullptr;
-        HIP_TRY(ctx, hipMalloc(&np, offset + bytes), "hipMalloc(buffer grow)");
+        Buffer nb;
+        HIP_TRY(ctx, skewed_alloc(nb, offset + bytes), "hipMalloc(buffer grow)");
         if (b->ptr && b->bytes) {
-            hipError_t e = hipMemcpyAsync(np, b->ptr, b->bytes, hipMemcpyDeviceToDevice, ctx->stream);
+            hipError_t e = hipMemcpyAsync(nb.ptr, b->ptr, b->bytes, hipMemcpyDeviceToDevice, ctx->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
             if (e != hipSuccess) {
-                (void)hipFree(np);
+                (void)hipFree(nb.raw);
                 return hip_fail(ctx, e, "buffer grow copy");
             }
-            (void)hipFree(b->ptr);
         }
-        b->ptr = np;
-        b->bytes = offset + bytes;
+        if (b->raw) (void)hipFree(b->raw);
+        *b = nb;
     }
     if (bytes) {
         HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(b->ptr) + offset, src, bytes, hipMemcpyHostToDevice, ctx->stream),
@@ -397,7 +420,7 @@ int wcpt_buffer_free(wcpt_context* ctx, wcpt_buffer buf)
     auto it = ctx->buffers.find(buf);
     if (it == ctx->buffers.end()) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(free)");
-    if (it->second.ptr) HIP_TRY(ctx, hipFree(it->second.ptr), "hipFree");
+    if (it->second.raw) HIP_TRY(ctx, hipFree(it->second.raw), "hipFree");
     ctx->buffers.erase(it);
     return WCPT_SUCCESS;
 }
@@ -533,6 +556,19 @@ int wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64
     out->wave_segment_steps = h[12];
     out->lane_segment_steps = h[13];
     return read_status(ctx);
+}
+
+int wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!out || n > 8) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_read_diagnostics: bad output");
+    memset(out, 0, sizeof(uint64_t) * n);
+    if (!ctx->wf.diag || n == 0) return WCPT_SUCCESS;
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wf.diag, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream),
+            "hipMemcpyAsync(diag)");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    return WCPT_SUCCESS;
 }
 
 /* ---- timing --------------------------------------------------------------------------------------- */

@@ -40,6 +40,7 @@ KERNEL_WAVEFRONT = 2
 
 OPTION_STACK = 1
 OPTION_DIAGNOSTICS = 2
+OPTION_SORT_RAYS = 3
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
@@ -119,6 +120,7 @@ _PROTOTYPES = {
     "wcpt_render": (_i, [_p, _p, _u64, _u64, _u64]),
     "wcpt_sync": (_i, [_p]),
     "wcpt_render_counters": (_i, [_p, _p, _u64, _u64, _u64, C.POINTER(Counters)]),
+    "wcpt_read_diagnostics": (_i, [_p, C.POINTER(C.c_uint64), _u32]),
     "wcpt_profile_begin": (_i, [_p]),
     "wcpt_profile_end": (_i, [_p, C.POINTER(C.c_double), C.POINTER(_u32)]),
     "wcpt_obj_parse": (_i, [C.c_char_p, _u64, C.POINTER(Mesh)]),

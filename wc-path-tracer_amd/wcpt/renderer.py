@@ -141,6 +141,11 @@ class Context:
             lib.wcpt_set_option(self.h, OPTION_DIAGNOSTICS, 0)
         return c.as_dict(diagnostics)
 
+    def read_diagnostics(self) -> list:
+        out = (C.c_uint64 * 8)()
+        self._chk(lib.wcpt_read_diagnostics(self.h, out, 8))
+        return [int(v) for v in out]
+
     def profile_begin(self):
         self._chk(lib.wcpt_profile_begin(self.h))
 
