@@ -38,6 +38,10 @@ CONFIGS = {
     "c4": ("atrium", 3840, 2160, 16, 4, "Sponza-scale atrium OBJ (262k tris), 3840x2160, 16 spp, 4 bounces"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# Measured best kernel per workload: the megakernel wins on the coherent, L1-resident
+# Cornell box; the wavefront variant wins on the 262k-triangle atrium (incoherent, MALL-resident).
+DEFAULT_KERNEL = {"c1": wcpt.KERNEL_MEGAKERNEL, "c2": wcpt.KERNEL_MEGAKERNEL, "c3": wcpt.KERNEL_WAVEFRONT,
+                  "c4": wcpt.KERNEL_WAVEFRONT}
 
 
 def algorithmic_bytes(c: dict) -> int:
@@ -84,7 +88,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", type=int, default=wcpt.KERNEL_MEGAKERNEL)
+    ap.add_argument("--kernel", type=int, default=-1,
+                    help="0 megakernel, 2 wavefront, -1 per-config default (DEFAULT_KERNEL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -99,6 +104,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     name, W, H, spp, bounces, desc = CONFIGS[args.config]
+    if args.kernel < 0:
+        args.kernel = DEFAULT_KERNEL[args.config]
     scene = wscene.generate(name)
     y0, rows = row_block(H, world, rank)
     stream = torch.cuda.current_stream()

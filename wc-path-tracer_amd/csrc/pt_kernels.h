@@ -64,7 +64,9 @@ constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream);
 /* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
-hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, hipStream_t stream);
+/* lds_stack: LDS traversal-stack entries per lane of the trace kernel (10, 16 or 24; render mode only). */
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, int lds_stack,
+                            hipStream_t stream);
 hipError_t wf_reserve(WfState& s, uint32_t paths);
 void wf_release(WfState& s);
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n,

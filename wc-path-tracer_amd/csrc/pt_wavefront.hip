@@ -116,8 +116,11 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
  * once per ray in the epilogue with the reference's expressions (:145, :173), which gives bit-identical
  * values. With the 10-entry LDS stack (5 KiB/wave) and __launch_bounds__(64, 8) the kernel runs 8 waves per
  * SIMD (32 per CU) to keep more dependent node fetches in flight. */
-constexpr int kWfLdsStack = 10;
-constexpr int kWfSpill = kStackDepth - kWfLdsStack;
+/* LDS per wave: the traversal stack, n entries per lane, 8 B each, lane-interleaved. n = 10 -> 5 KiB/wave,
+ * 8 waves/SIMD; 16 -> 5 waves; 24 -> 3 waves. Deeper entries spill to scratch (measured on c3: 10 and 16
+ * entries run within 1%, 24 is 13% slower -- the traversal is bound by node-fetch latency, not the spill). */
+constexpr int wf_lds_per_wave(int n) { return n * 512; }
+constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
 constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
@@ -158,16 +161,16 @@ __device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, uint3
     mode = count > 0 ? kModeLeaf : kModeInterior;
 }
 
-template <bool COUNT, bool DIAG, bool SINGLE>
-__global__ __launch_bounds__(64, 8) void wf_trace(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
+template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
+__global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
                                                   const wcpt_draw_command* __restrict__ draws, WfBuffers b,
                                                   uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
 {
-    __shared__ uint2 s_stack[kWfLdsStack * 64];
+    __shared__ uint2 s_stack[LDSN * 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.count_out = 0; /* shade appends to it after this kernel */
     const uint32_t n = *b.count_in;
     const uint32_t lane = lane_id();
-    LdsStack<kWfLdsStack, kWfSpill> stk;
+    LdsStack<LDSN, kStackDepth - LDSN> stk;
     stk.base = s_stack + lane;
     Counters cnt = {};
     bool overflow = false;
@@ -543,20 +546,43 @@ __global__ __launch_bounds__(256) void wf_sort_keys(WfBuffers b, uint32_t P, con
     }
 }
 
-template <bool COUNT, bool DIAG, bool SINGLE>
+template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
 static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace_grid, uint32_t shade_grid,
                          hipStream_t stream)
 {
-    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.spheres,
+    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.spheres,
                        a.draws, b, a.status, a.counters);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials, b,
                        a.image, a.W, a.H, a.y0, a.counters);
 }
 
-template <bool COUNT, bool DIAG, bool SINGLE>
+template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
 static hipError_t trace_blocks_per_cu(int& bpc)
 {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<COUNT, DIAG, SINGLE>, 64, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>, 64, 0);
+}
+
+/* One (mode, single-draw, LDS depth) instantiation: occupancy query or one trace+shade iteration. */
+template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
+static hipError_t wf_variant(bool query, int& bpc, const LaunchArgs& a, const WfBuffers& b, uint32_t trace_grid,
+                             uint32_t shade_grid, hipStream_t stream)
+{
+    if (query) return trace_blocks_per_cu<COUNT, DIAG, SINGLE, LDSN>(bpc);
+    wf_iteration<COUNT, DIAG, SINGLE, LDSN>(a, b, trace_grid, shade_grid, stream);
+    return hipGetLastError();
+}
+
+static hipError_t wf_dispatch(int mode, bool single, int ldsn, bool query, int& bpc, const LaunchArgs& a,
+                              const WfBuffers& b, uint32_t tg, uint32_t sg, hipStream_t st)
+{
+    if (mode == kModeCount) return single ? wf_variant<true, false, true, 10>(query, bpc, a, b, tg, sg, st)
+                                          : wf_variant<true, false, false, 10>(query, bpc, a, b, tg, sg, st);
+    if (mode == kModeDiag) return single ? wf_variant<true, true, true, 10>(query, bpc, a, b, tg, sg, st)
+                                         : wf_variant<true, true, false, 10>(query, bpc, a, b, tg, sg, st);
+    if (!single) return wf_variant<false, false, false, 10>(query, bpc, a, b, tg, sg, st);
+    if (ldsn == 16) return wf_variant<false, false, true, 16>(query, bpc, a, b, tg, sg, st);
+    if (ldsn == 24) return wf_variant<false, false, true, 24>(query, bpc, a, b, tg, sg, st);
+    return wf_variant<false, false, true, 10>(query, bpc, a, b, tg, sg, st);
 }
 
 static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b, uint32_t P, int cus,
@@ -573,7 +599,7 @@ static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b
     return hipMemcpyAsync(b.queue_in, s.sort_vals, (size_t)P * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
 }
 
-hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, hipStream_t stream)
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, int lds_stack, hipStream_t stream)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tilesY = (a.rows + 7u) / 8u;
@@ -589,12 +615,11 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
     const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
-    static int trace_bpc[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-    int& bpc = trace_bpc[mode][single ? 1 : 0];
+    const int ldsn = (lds_stack == 16 || lds_stack == 24) ? lds_stack : 10;
+    static int trace_bpc[3][2][3] = {};
+    int& bpc = trace_bpc[mode][single ? 1 : 0][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
     if (bpc == 0) {
-        if (mode == kModeRender) e = single ? trace_blocks_per_cu<false, false, true>(bpc) : trace_blocks_per_cu<false, false, false>(bpc);
-        else if (mode == kModeCount) e = single ? trace_blocks_per_cu<true, false, true>(bpc) : trace_blocks_per_cu<true, false, false>(bpc);
-        else e = single ? trace_blocks_per_cu<true, true, true>(bpc) : trace_blocks_per_cu<true, true, false>(bpc);
+        e = wf_dispatch(mode, single, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);
         if (e != hipSuccess) return e;
         if (bpc < 1) bpc = 1;
     }
@@ -630,16 +655,8 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
             e = sort_queue(a, s, b, P, cus, stream);
             if (e != hipSuccess) return e;
         }
-        if (single) {
-            if (mode == kModeRender) wf_iteration<false, false, true>(a, b, trace_grid, shade_grid, stream);
-            else if (mode == kModeCount) wf_iteration<true, false, true>(a, b, trace_grid, shade_grid, stream);
-            else wf_iteration<true, true, true>(a, b, trace_grid, shade_grid, stream);
-        } else {
-            if (mode == kModeRender) wf_iteration<false, false, false>(a, b, trace_grid, shade_grid, stream);
-            else if (mode == kModeCount) wf_iteration<true, false, false>(a, b, trace_grid, shade_grid, stream);
-            else wf_iteration<true, true, false>(a, b, trace_grid, shade_grid, stream);
-        }
-        e = hipGetLastError();
+        int unused = 0;
+        e = wf_dispatch(mode, single, ldsn, false, unused, a, b, trace_grid, shade_grid, stream);
         if (e != hipSuccess) return e;
         std::swap(b.queue_in, b.queue_out);
         std::swap(b.count_in, b.count_out);

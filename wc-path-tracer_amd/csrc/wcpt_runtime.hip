@@ -74,6 +74,7 @@ struct wcpt_context {
     int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + scratch spill */
     int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
+    int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     std::string last_error;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -196,7 +197,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
     case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->stream); break;
-    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->sort_rays != 0, ctx->stream); break;
+    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream); break;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
@@ -320,6 +321,11 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     switch (option) {
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_WF_STACK:
+        if (value != 10 && value != 16 && value != 24)
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wavefront LDS stack %d (10, 16 or 24)", value);
+        ctx->wf_stack = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_DIAGNOSTICS:
         ctx->diagnostics = value ? 1 : 0;
