@@ -201,44 +201,51 @@ __device__ __forceinline__ void simd_step(uint32_t& wave, uint32_t& lane_steps)
  * that the per-XCD L2 cannot hold at full occupancy (measured: ~6 GB of writes per 1080p atrium frame).
  * LdsStack keeps the first N entries in LDS, lane-interleaved ([entry][64 lanes] of 8-byte words: one
  * conflict-free ds_write_b64 / ds_read_b64 per wave), and only entries N..N+SPILL-1 in scratch. */
+/* The entry storage is a separate private array owned by the caller (`mem` / `spill` point at it) so that the
+ * stack pointer itself stays in a register: with the arrays inside the struct, the dynamic array indexing kept
+ * the whole struct -- sp included -- in scratch, and every push/pop paid a scratch round trip for sp. */
+typedef __attribute__((address_space(5))) uint64_t* priv_u64_ptr;
+typedef __attribute__((address_space(3))) uint64_t* lds_u64_ptr;
+
 template <int N>
 struct PrivateStack {
-    uint32_t idx[N];
-    float t0[N];
+    priv_u64_ptr mem; /* caller's private uint64_t[N], entries (node index | t0 bits << 32) */
     int sp;
     __device__ __forceinline__ void reset() { sp = 0; }
     __device__ __forceinline__ bool empty() const { return sp == 0; }
     __device__ __forceinline__ bool push(uint32_t i, float t)
     {
         if (sp >= N) return false;
-        idx[sp] = i;
-        t0[sp] = t;
+        mem[sp] = (uint64_t)i | ((uint64_t)__float_as_uint(t) << 32);
         sp++;
         return true;
     }
     __device__ __forceinline__ void pop(uint32_t& i, float& t)
     {
         sp--;
-        i = idx[sp];
-        t = t0[sp];
+        const uint64_t e = mem[sp];
+        i = (uint32_t)e;
+        t = __uint_as_float((uint32_t)(e >> 32));
     }
 };
 
+/* Entries are packed (node index | t0 bits << 32). The two storage classes are typed by address space so that
+ * the compiler emits ds_read/ds_write for the LDS part and scratch_* for the spill instead of merging the two
+ * into one flat access. */
 template <int N, int SPILL>
 struct LdsStack {
-    uint2* base; /* &lds[0][lane] */
-    uint32_t sidx[SPILL];
-    float st0[SPILL];
+    lds_u64_ptr base;   /* &lds[0][lane] */
+    priv_u64_ptr spill; /* caller's private uint64_t[SPILL] */
     int sp;
     __device__ __forceinline__ void reset() { sp = 0; }
     __device__ __forceinline__ bool empty() const { return sp == 0; }
     __device__ __forceinline__ bool push(uint32_t i, float t)
     {
+        const uint64_t e = (uint64_t)i | ((uint64_t)__float_as_uint(t) << 32);
         if (sp < N) {
-            base[sp * 64] = make_uint2(i, __float_as_uint(t));
+            base[sp * 64] = e;
         } else if (sp < N + SPILL) {
-            sidx[sp - N] = i;
-            st0[sp - N] = t;
+            spill[sp - N] = e;
         } else {
             return false;
         }
@@ -248,14 +255,13 @@ struct LdsStack {
     __device__ __forceinline__ void pop(uint32_t& i, float& t)
     {
         sp--;
-        if (sp < N) {
-            const uint2 e = base[sp * 64];
-            i = e.x;
-            t = __uint_as_float(e.y);
-        } else {
-            i = sidx[sp - N];
-            t = st0[sp - N];
-        }
+        uint64_t e;
+        if (sp < N)
+            e = base[sp * 64];
+        else
+            e = spill[sp - N];
+        i = (uint32_t)e;
+        t = __uint_as_float((uint32_t)(e >> 32));
     }
 };
 

@@ -86,12 +86,16 @@ __global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, co
     bool overflow = false;
     if (lx < W && ly < rows) {
         if constexpr (SK == 0) {
+            uint64_t mem[kPrivateStack];
             PrivateStack<kPrivateStack> stk;
+            stk.mem = (priv_u64_ptr)mem;
             shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, image, W, H, y0, lx, ly, stk, cnt, overflow);
         } else {
-            __shared__ uint2 s_stack[kLdsStack * 64];
+            __shared__ uint64_t s_stack[kLdsStack * 64];
+            uint64_t spill[kSpillStack];
             LdsStack<kLdsStack, kSpillStack> stk;
-            stk.base = s_stack + (threadIdx.x & 63u);
+            stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
+            stk.spill = (priv_u64_ptr)spill;
             shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, image, W, H, y0, lx, ly, stk, cnt, overflow);
         }
     }

@@ -166,12 +166,15 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                                                   const wcpt_draw_command* __restrict__ draws, WfBuffers b,
                                                   uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
 {
-    __shared__ uint2 s_stack[LDSN * 64];
+    __shared__ uint64_t s_stack[LDSN * 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.count_out = 0; /* shade appends to it after this kernel */
     const uint32_t n = *b.count_in;
     const uint32_t lane = lane_id();
+    uint64_t spill[kStackDepth - LDSN];
     LdsStack<LDSN, kStackDepth - LDSN> stk;
-    stk.base = s_stack + lane;
+    stk.base = (lds_u64_ptr)(s_stack + lane);
+    stk.spill = (priv_u64_ptr)spill;
+    stk.sp = 0;
     Counters cnt = {};
     bool overflow = false;
     Geom g0 = {nullptr, nullptr, nullptr}, gl = {nullptr, nullptr, nullptr};
