@@ -35,8 +35,9 @@ struct WfBuffers {
     float4* light;     /* (totalLight.xyz, rng state bits)                */
     float4* trans;     /* (transmittance.xyz, -)                          */
     float4* result;    /* (sum of sample radiance .xyz, -)                */
-    float4* hit;       /* (t, normal.xyz) of the last Intersect            */
-    uint2* hitinfo;    /* (material, flags)                               */
+    float4* pre;       /* (invDirection.xyz, t of the sphere loop) of the queued ray          */
+    uint32_t* pre_prim;/* sphere loop's winner (kSpherePrim | i) or kNoPrim                  */
+    float4* hit;       /* (t, primitive bits, draw bits, -) of the last Intersect             */
     uint32_t* queue_in;
     uint32_t* count_in;
     uint32_t* queue_out;
@@ -48,7 +49,8 @@ struct WfState {
     void* mem = nullptr;
     uint32_t capacity = 0;
     float4 *ray0 = nullptr, *ray1 = nullptr, *light = nullptr, *trans = nullptr, *result = nullptr, *hit = nullptr;
-    uint2* hitinfo = nullptr;
+    float4* pre = nullptr;
+    uint32_t* pre_prim = nullptr;
     uint32_t* queue[2] = {nullptr, nullptr};
     uint32_t* ctr = nullptr;
     unsigned long long* diag = nullptr;

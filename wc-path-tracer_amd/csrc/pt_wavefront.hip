@@ -18,7 +18,12 @@
  * The host runs trace+shade samples*(maxBounceCount+1) times (each iteration advances every live path by
  * exactly one segment). Each path executes exactly the megakernel's operation sequence (same traversal
  * order, same RNG stream), so the image is bit-identical; only the order in which paths are processed
- * changes. Path state lives in HBM as structure-of-arrays float4s (80 B/path + 24 B hit record).
+ * changes. Path state lives in HBM as structure-of-arrays float4s (112 B/path + 4 B sphere-loop winner).
+ *
+ * Everything of Intersect that does not depend on the BVH runs where every lane is busy: the sphere loop
+ * (:136-149) and 1/direction run in the kernel that creates the ray (wf_init / wf_shade) and travel with it
+ * in `pre`; the winner's normal, facing and material (:145, :173, :204-208) are rebuilt in wf_shade from the
+ * (t, primitive) record the trace kernel leaves. The divergent trace loop keeps only the BVH walk.
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -32,16 +37,36 @@ namespace dev {
 constexpr uint32_t kTraceChunk = 64;   /* queue entries a wave claims per atomicAdd */
 constexpr int kShadeBlock = 256;
 
-/* Hit record flags */
-constexpr uint32_t kHitFlag = 1u, kFrontFlag = 2u;
+constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
-__device__ __forceinline__ void store_ray(const WfBuffers& b, uint32_t p, const Ray& r, uint32_t bounce, uint32_t sample)
+/* Queue a ray for the next trace: its state plus the Intersect prologue (:136-149, the sphere loop) and
+ * 1/direction, computed here with all lanes busy. Counts the segment (one Intersect call per queued ray). */
+template <bool COUNT>
+__device__ __forceinline__ void store_segment(const WfBuffers& b, uint32_t p, const Ray& r, uint32_t bounce,
+                                              uint32_t sample, const wcpt_scene_data& sd,
+                                              const wcpt_sphere* __restrict__ spheres, Counters& cnt)
 {
     b.ray0[p] = make_float4(r.origin.x, r.origin.y, r.origin.z, r.direction.x);
     b.ray1[p] = make_float4(r.direction.y, r.direction.z, __uint_as_float(bounce), __uint_as_float(sample));
+    float rt = kInfinity;
+    uint32_t prim = kNoPrim;
+    for (uint32_t i = 0; i < sd.sphereCount; i++) {
+        const wcpt_sphere& s = spheres[i];
+        const float tempRec = raySphereNear(r, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
+        if (tempRec > 0.0f && tempRec < rt) {
+            rt = tempRec;
+            prim = kSpherePrim | i;
+        }
+    }
+    if (COUNT) {
+        cnt.segments++;
+        cnt.sphere_tests += sd.sphereCount;
+    }
+    b.pre[p] = make_float4(r.invDirection.x, r.invDirection.y, r.invDirection.z, rt);
+    b.pre_prim[p] = prim;
 }
 
 /* Block-aggregated append of `pred` lanes to a queue: one atomicAdd per block. All threads of the block must
@@ -69,7 +94,8 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 
 /* ---- ray generation ------------------------------------------------------------------------------- */
 template <bool COUNT>
-__global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd, WfBuffers b, float4* __restrict__ image,
+__global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
+                                                       WfBuffers b, float4* __restrict__ image,
                                                        uint32_t W, uint32_t H, uint32_t y0, uint32_t rows,
                                                        uint32_t tilesX, uint32_t total,
                                                        unsigned long long* __restrict__ counters)
@@ -93,7 +119,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
                     PathState ps;
                     path_begin(ps, mk3(sd.position[0], sd.position[1], sd.position[2]),
                                primary_direction(sd, lx, y, W, H));
-                    store_ray(b, p, ps.ray, 0u, 0u);
+                    store_segment<COUNT>(b, p, ps.ray, 0u, 0u, sd, spheres, cnt);
                     b.light[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(seed));
                     b.trans[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
                     live = true;
@@ -107,7 +133,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
         const uint32_t slot = block_append(b.count_in, live, s_wave, &s_base);
         if (live) b.queue_in[slot] = p;
     }
-    if (COUNT) wave_add_u64(&counters[0], cnt.pixels);
+    flush_counters<COUNT>(cnt, counters);
 }
 
 /* ---- trace ------------------------------------------------------------------------------------------ */
@@ -122,7 +148,6 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
 constexpr int wf_lds_per_wave(int n) { return n * 512; }
 constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
-constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
 struct Geom {
     gnode_ptr bvh;
@@ -162,7 +187,7 @@ __device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, uint3
 }
 
 template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
-__global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
+__global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
                                                   const wcpt_draw_command* __restrict__ draws, WfBuffers b,
                                                   uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
 {
@@ -214,7 +239,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 if (lo == hi) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(b.head, kTraceChunk);
-                    base = __shfl(base, 0, 64);
+                    base = __builtin_amdgcn_readfirstlane(base); /* wave-uniform: keeps lo/hi in SGPRs */
                     if (base >= n) {
                         drained = true;
                         break;
@@ -227,26 +252,13 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 const bool take = ((need >> lane) & 1ull) && rank < avail;
                 if (take) {
                     p = b.queue_in[lo + rank];
-                    const float4 r0 = b.ray0[p], r1 = b.ray1[p];
+                    const float4 r0 = b.ray0[p], r1 = b.ray1[p], pr = b.pre[p];
                     ray.origin = mk3(r0.x, r0.y, r0.z);
                     ray.direction = mk3(r0.w, r1.x, r1.y);
-                    ray.invDirection = rcp3(ray.direction);
-                    /* Intersect prologue (:136-149): the sphere loop */
-                    rt = kInfinity;
-                    prim = kNoPrim;
-                    if (COUNT) {
-                        cnt.segments++;
-                        simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
-                    }
-                    for (uint32_t i = 0; i < sd.sphereCount; i++) {
-                        const wcpt_sphere& s = spheres[i];
-                        const float tempRec = raySphereNear(ray, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
-                        if (COUNT) cnt.sphere_tests++;
-                        if (tempRec > 0.0f && tempRec < rt) {
-                            rt = tempRec;
-                            prim = kSpherePrim | i;
-                        }
-                    }
+                    ray.invDirection = mk3(pr.x, pr.y, pr.z);
+                    rt = pr.w;                /* sphere loop (:136-149), run by the ray's creator */
+                    prim = b.pre_prim[p];
+                    if (COUNT) simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
                     d = 0;
                     start_draw();
                     has = true;
@@ -327,31 +339,8 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             }
             diag_mark<DIAG>(tim, tprev, 3);
             if (has && mode == kModeDone) {
-                /* Intersect epilogue (:204-208), with the winner's normal and material rebuilt as at :145/:173 */
-                uint32_t flags = 0, mat = 0;
-                f3 nrm = mk3(0.0f, 0.0f, 0.0f);
-                if (prim != kNoPrim) {
-                    if (prim & kSpherePrim) {
-                        const wcpt_sphere& s = spheres[prim & ~kSpherePrim];
-                        const f3 c = mk3(s.position[0], s.position[1], s.position[2]);
-                        const f3 ph = ray.origin + rt * ray.direction;
-                        nrm = (ph - c) / s.radius;
-                        mat = s.material;
-                    } else {
-                        const Geom gw = SINGLE ? g0 : load_geom(draws, primDraw);
-                        const f3 a = ld3(gw.vertices + 3ull * gw.indices[prim + 0]);
-                        const f3 bb = ld3(gw.vertices + 3ull * gw.indices[prim + 1]);
-                        const f3 c = ld3(gw.vertices + 3ull * gw.indices[prim + 2]);
-                        nrm = normalize(cross(bb - a, c - a));
-                        mat = 0; /* :175 */
-                    }
-                    const bool front = dot(ray.direction, nrm) < 0.0f;
-                    if (!front) nrm = nrm * -1.0f;
-                    flags = kHitFlag | (front ? kFrontFlag : 0u);
-                    if (COUNT) cnt.hits++;
-                }
-                b.hit[p] = make_float4(rt, nrm.x, nrm.y, nrm.z);
-                b.hitinfo[p] = make_uint2(mat, flags);
+                /* Intersect result; wf_shade rebuilds the winner's normal and material (:204-208) */
+                b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
                 has = false;
             }
             diag_mark<DIAG>(tim, tprev, 4);
@@ -368,7 +357,8 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
 /* ---- shade ------------------------------------------------------------------------------------------ */
 template <bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
-                                                        WfBuffers b, float4* __restrict__ image, uint32_t W,
+                                                        const wcpt_sphere* __restrict__ spheres,
+                                                        const wcpt_draw_command* __restrict__ draws, WfBuffers b, float4* __restrict__ image, uint32_t W,
                                                         uint32_t H, uint32_t y0, unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_wave[kShadeBlock / 64], s_base;
@@ -382,22 +372,43 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
         if (w < n) {
             p = b.queue_in[w];
             const float4 r0 = b.ray0[p], r1 = b.ray1[p], li = b.light[p], tr = b.trans[p], hi = b.hit[p];
-            const uint2 hf = b.hitinfo[p];
             PathState ps;
             ps.ray.origin = mk3(r0.x, r0.y, r0.z);
             ps.ray.direction = mk3(r0.w, r1.x, r1.y);
-            ps.ray.invDirection = rcp3(ps.ray.direction);
             ps.totalLight = mk3(li.x, li.y, li.z);
             ps.transmittance = mk3(tr.x, tr.y, tr.z);
             ps.bounce = __float_as_uint(r1.z);
             uint32_t sample = __float_as_uint(r1.w);
             uint32_t seed = __float_as_uint(li.w);
+            /* Intersect epilogue (:204-208): the winner's normal and material, rebuilt with the expressions of
+             * :145 (sphere) and :173-175 (triangle), then the facing flip */
             Hit h;
-            h.hit = (hf.y & kHitFlag) != 0u;
-            h.front = (hf.y & kFrontFlag) != 0u;
-            h.material = hf.x;
+            const uint32_t prim = __float_as_uint(hi.y);
             h.t = hi.x;
-            h.normal = mk3(hi.y, hi.z, hi.w);
+            h.hit = prim != kNoPrim;
+            h.front = false;
+            h.material = 0;
+            h.normal = mk3(0.0f, 0.0f, 0.0f);
+            if (h.hit) {
+                if (prim & kSpherePrim) {
+                    const wcpt_sphere& s = spheres[prim & ~kSpherePrim];
+                    const f3 c = mk3(s.position[0], s.position[1], s.position[2]);
+                    const f3 ph = ps.ray.origin + h.t * ps.ray.direction;
+                    h.normal = (ph - c) / s.radius;
+                    h.material = s.material;
+                } else {
+                    const wcpt_draw_command& dc = draws[__float_as_uint(hi.z)];
+                    const gu32_ptr idx = as_u32(dc.indexBuffer);
+                    const gf32_ptr vtx = as_f32(dc.vertexBuffer);
+                    const f3 a = ld3(vtx + 3ull * idx[prim + 0]);
+                    const f3 bb = ld3(vtx + 3ull * idx[prim + 1]);
+                    const f3 c = ld3(vtx + 3ull * idx[prim + 2]);
+                    h.normal = normalize(cross(bb - a, c - a));
+                }
+                h.front = dot(ps.ray.direction, h.normal) < 0.0f;
+                if (!h.front) h.normal = h.normal * -1.0f;
+                if (COUNT) cnt.hits++;
+            }
             h.p = ps.ray.origin + h.t * ps.ray.direction; /* :205 */
             f3 L;
             if (!path_shade(ps, h, seed, sd, mats, L)) {
@@ -432,7 +443,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
                 }
             }
             if (cont) {
-                store_ray(b, p, ps.ray, ps.bounce, sample);
+                store_segment<COUNT>(b, p, ps.ray, ps.bounce, sample, sd, spheres, cnt);
                 b.light[p] = make_float4(ps.totalLight.x, ps.totalLight.y, ps.totalLight.z, __uint_as_float(seed));
                 b.trans[p] = make_float4(ps.transmittance.x, ps.transmittance.y, ps.transmittance.z, 0.0f);
             }
@@ -440,7 +451,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
         const uint32_t slot = block_append(b.count_out, cont, s_wave, &s_base);
         if (cont) b.queue_out[slot] = p;
     }
-    if (COUNT) wave_add_u64(&counters[0], cnt.pixels);
+    flush_counters<COUNT>(cnt, counters);
 }
 
 } // namespace dev
@@ -465,7 +476,7 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     if (paths <= s.capacity) return hipSuccess;
     wf_release(s);
     const size_t P = paths;
-    const size_t bytes = P * (6 * sizeof(float4) + sizeof(uint2) + 2 * sizeof(uint32_t)) + 256;
+    const size_t bytes = P * (7 * sizeof(float4) + 3 * sizeof(uint32_t)) + 256;
     char* m = nullptr;
     hipError_t e = hipMalloc(&m, bytes);
     if (e != hipSuccess) return e;
@@ -477,8 +488,9 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     s.trans = f + 3 * P;
     s.result = f + 4 * P;
     s.hit = f + 5 * P;
-    s.hitinfo = reinterpret_cast<uint2*>(f + 6 * P);
-    s.queue[0] = reinterpret_cast<uint32_t*>(s.hitinfo + P);
+    s.pre = f + 6 * P;
+    s.pre_prim = reinterpret_cast<uint32_t*>(f + 7 * P);
+    s.queue[0] = s.pre_prim + P;
     s.queue[1] = s.queue[0] + P;
     s.ctr = s.queue[1] + P; /* [0] count q0, [1] count q1, [2] trace head */
     s.diag = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(s.ctr + 4 + 7) & ~uintptr_t(7));
@@ -553,10 +565,10 @@ template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
 static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace_grid, uint32_t shade_grid,
                          hipStream_t stream)
 {
-    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.spheres,
-                       a.draws, b, a.status, a.counters);
-    hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials, b,
-                       a.image, a.W, a.H, a.y0, a.counters);
+    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
+                       b, a.status, a.counters);
+    hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
+                       a.spheres, a.draws, b, a.image, a.W, a.H, a.y0, a.counters);
 }
 
 template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
@@ -633,7 +645,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     if (e != hipSuccess) return e;
     WfBuffers b;
     b.ray0 = s.ray0; b.ray1 = s.ray1; b.light = s.light; b.trans = s.trans; b.result = s.result;
-    b.hit = s.hit; b.hitinfo = s.hitinfo; b.head = s.ctr + 2; b.diag = s.diag;
+    b.hit = s.hit; b.pre = s.pre; b.pre_prim = s.pre_prim; b.head = s.ctr + 2; b.diag = s.diag;
     if (mode == kModeDiag) {
         e = hipMemsetAsync(s.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
@@ -642,10 +654,10 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     b.queue_out = s.queue[1]; b.count_out = s.ctr + 1;
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);
     if (count)
-        hipLaunchKernelGGL(dev::wf_init<true>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, b, a.image,
+        hipLaunchKernelGGL(dev::wf_init<true>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
                            a.W, a.H, a.y0, a.rows, tilesX, total, a.counters);
     else
-        hipLaunchKernelGGL(dev::wf_init<false>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, b, a.image,
+        hipLaunchKernelGGL(dev::wf_init<false>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
                            a.W, a.H, a.y0, a.rows, tilesX, total, a.counters);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
