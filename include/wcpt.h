@@ -59,7 +59,7 @@ extern "C" {
 #define WCPT_KERNEL_WAVEFRONT   2  /* split ray-gen / traverse / shade queues (same semantics)         */
 
 /* ---- tuning options (wcpt_set_option); none changes results ------------------------------------- */
-#define WCPT_OPTION_STACK       1  /* traversal stack: 0 = scratch, 1 = LDS + scratch spill (default)   */
+#define WCPT_OPTION_STACK       1  /* megakernel traversal stack: 0 = scratch (default), 1 = LDS + spill */
 #define WCPT_OPTION_DIAGNOSTICS 2  /* 1: wcpt_render_counters also fills the SIMD-efficiency fields      */
 #define WCPT_OPTION_SORT_RAYS   3  /* wavefront: sort bounce rays by (octant, origin Morton) (default 0) */
 #define WCPT_OPTION_WF_STACK    4  /* wavefront: LDS traversal-stack entries per lane, 10 | 16 | 24 (default 10) */

@@ -54,7 +54,7 @@ def main():
     for r in range(a.rounds + 1):
         for v in a.variants:
             o = parse(v)
-            ctx.set_option(wcpt._lib.OPTION_STACK, int(o.get("stack", 1)))
+            ctx.set_option(wcpt._lib.OPTION_STACK, int(o.get("stack", 0)))
             ctx.set_kernel(int(o.get("kernel", 0)))
             ctx.set_option(wcpt._lib.OPTION_SORT_RAYS, int(o.get("sort", 0)))
             ctx.set_option(wcpt._lib.OPTION_WF_STACK, int(o.get("lds", 10)))

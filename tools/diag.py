@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--kernel", type=int, default=0)
-    ap.add_argument("--stack", type=int, default=1)
+    ap.add_argument("--stack", type=int, default=0)
     ap.add_argument("--size", default=None, help="WxH override")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]

@@ -9,7 +9,7 @@
  *   - SceneData is a kernel argument (scalar loads from the kernarg segment) instead of a BDA buffer.
  *   - BVH traversal keeps the nearer child in registers and pushes only the farther one, with the box
  *     entry distance t0 on the stack. A child whose box test fails statically (t0 > t1 || t1 < 0) is never
- *     pushed; the dynamic cull (t0 > rec.t) is applied when the child would have been popped. This is
+ *     pushed; the dynamic cull (t0 > rt) is applied when the child would have been popped. This is
  *     exactly the reference's pop order and cull set (pathTracer.comp:157-200) with one 64-byte sibling
  *     fetch per interior node instead of 32 (pop) + 64 (children) bytes.
  */
@@ -265,19 +265,53 @@ struct LdsStack {
     }
 };
 
+/* Closest-hit record during traversal: (t, primitive) only; the winner's normal and material are rebuilt
+ * once afterwards (resolve_hit) with the reference's expressions, which gives the values the reference
+ * computes at each update (:145, :173) without paying a normalize per closer hit. */
+constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
+
+/* Intersect epilogue (:204-208) for winner `prim` (kNoPrim, kSpherePrim | sphere, or the index position of
+ * a triangle of draw `draw`) at distance t. */
+__device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t prim, uint32_t draw,
+                                           const wcpt_sphere* __restrict__ spheres,
+                                           const wcpt_draw_command* __restrict__ draws)
+{
+    Hit h;
+    h.t = t;
+    h.hit = prim != kNoPrim;
+    h.front = false;
+    h.material = 0;
+    h.normal = mk3(0.0f, 0.0f, 0.0f);
+    if (h.hit) {
+        if (prim & kSpherePrim) {
+            const wcpt_sphere& s = spheres[prim & ~kSpherePrim];
+            const f3 c = mk3(s.position[0], s.position[1], s.position[2]);
+            const f3 ph = ray.origin + t * ray.direction;
+            h.normal = (ph - c) / s.radius;                        /* :145 */
+            h.material = s.material;
+        } else {
+            const gu32_ptr idx = as_u32(draws[draw].indexBuffer);
+            const gf32_ptr vtx = as_f32(draws[draw].vertexBuffer);
+            const f3 a = ld3(vtx + 3ull * idx[prim + 0]);
+            const f3 b = ld3(vtx + 3ull * idx[prim + 1]);
+            const f3 c = ld3(vtx + 3ull * idx[prim + 2]);
+            h.normal = normalize(cross(b - a, c - a));                /* :173, material 0 (:175) */
+        }
+        h.front = dot(ray.direction, h.normal) < 0.0f;
+        if (!h.front) h.normal = h.normal * -1.0f;
+    }
+    h.p = ray.origin + t * ray.direction;                             /* :205 */
+    return h;
+}
+
 /* pathTracer.comp:135-211 */
 template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
                                          const wcpt_draw_command* __restrict__ draws, Stack& stk,
                                          Counters& cnt, bool& overflow)
 {
-    Hit rec;
-    rec.t = kInfinity;
-    rec.hit = false;
-    rec.front = false;
-    rec.material = 0;
-    rec.p = mk3(0.0f, 0.0f, 0.0f);
-    rec.normal = mk3(0.0f, 0.0f, 0.0f);
+    float rt = kInfinity;
+    uint32_t prim = kNoPrim, primDraw = 0;
     if (COUNT) {
         cnt.segments++;
         simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
@@ -288,12 +322,9 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         const f3 sp = mk3(s.position[0], s.position[1], s.position[2]);
         const float tempRec = raySphereNear(ray, sp, s.radius);
         if (COUNT) cnt.sphere_tests++;
-        if (tempRec > 0.0f && tempRec < rec.t) {
-            rec.t = tempRec;
-            rec.p = ray.origin + rec.t * ray.direction;
-            rec.normal = (rec.p - sp) / s.radius;
-            rec.hit = true;
-            rec.material = s.material;
+        if (tempRec > 0.0f && tempRec < rt) {
+            rt = tempRec;
+            prim = kSpherePrim | i;
         }
     }
 
@@ -307,7 +338,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         NodeV cur = load_node(bvh, 0);
         float c0, c1;
         node_box(ray, cur, c0, c1);
-        if (c0 > c1 || c1 < 0.0f || c0 > rec.t) continue;
+        if (c0 > c1 || c1 < 0.0f || c0 > rt) continue;
         uint32_t curLeft = cur.b.z, curCount = cur.b.w;
         stk.reset();
         for (;;) {
@@ -326,11 +357,10 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                         cnt.triangle_tests++;
                         simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
                     }
-                    if (t != -1.0f && t < rec.t) {
-                        rec.t = t;
-                        rec.normal = normalize(cross(b - a, c - a));
-                        rec.hit = true;
-                        rec.material = 0; /* :175 */
+                    if (t != -1.0f && t < rt) {
+                        rt = t;
+                        prim = first;
+                        primDraw = i;
                     }
                 }
             } else {
@@ -357,7 +387,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 const float nearT0 = leftFirst ? l0 : r0;
                 const float farT0 = leftFirst ? r0 : l0;
                 if (passFar && !stk.push(farIdx, farT0)) overflow = true;
-                if (passNear && !(nearT0 > rec.t)) {
+                if (passNear && !(nearT0 > rt)) {
                     const NodeV& N = leftFirst ? L : R;
                     curLeft = N.b.z;
                     curCount = N.b.w;
@@ -370,7 +400,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 uint32_t ni;
                 float t0;
                 stk.pop(ni, t0);
-                if (t0 > rec.t) continue;
+                if (t0 > rt) continue;
                 const uint2 lc = load_node_lc(bvh, ni);
                 curLeft = lc.x;
                 curCount = lc.y;
@@ -381,13 +411,8 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         }
     }
 
-    if (rec.hit) {
-        rec.p = ray.origin + rec.t * ray.direction;
-        rec.front = dot(ray.direction, rec.normal) < 0.0f;
-        if (!rec.front) rec.normal = rec.normal * -1.0f;
-        if (COUNT) cnt.hits++;
-    }
-    return rec;
+    if (COUNT && prim != kNoPrim) cnt.hits++;
+    return resolve_hit(ray, rt, prim, primDraw, spheres, draws);
 }
 
 /* pathTracer.comp:213-234 */

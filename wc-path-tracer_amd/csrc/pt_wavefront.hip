@@ -37,7 +37,6 @@ namespace dev {
 constexpr uint32_t kTraceChunk = 64;   /* queue entries a wave claims per atomicAdd */
 constexpr int kShadeBlock = 256;
 
-constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
@@ -380,36 +379,9 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
             ps.bounce = __float_as_uint(r1.z);
             uint32_t sample = __float_as_uint(r1.w);
             uint32_t seed = __float_as_uint(li.w);
-            /* Intersect epilogue (:204-208): the winner's normal and material, rebuilt with the expressions of
-             * :145 (sphere) and :173-175 (triangle), then the facing flip */
-            Hit h;
             const uint32_t prim = __float_as_uint(hi.y);
-            h.t = hi.x;
-            h.hit = prim != kNoPrim;
-            h.front = false;
-            h.material = 0;
-            h.normal = mk3(0.0f, 0.0f, 0.0f);
-            if (h.hit) {
-                if (prim & kSpherePrim) {
-                    const wcpt_sphere& s = spheres[prim & ~kSpherePrim];
-                    const f3 c = mk3(s.position[0], s.position[1], s.position[2]);
-                    const f3 ph = ps.ray.origin + h.t * ps.ray.direction;
-                    h.normal = (ph - c) / s.radius;
-                    h.material = s.material;
-                } else {
-                    const wcpt_draw_command& dc = draws[__float_as_uint(hi.z)];
-                    const gu32_ptr idx = as_u32(dc.indexBuffer);
-                    const gf32_ptr vtx = as_f32(dc.vertexBuffer);
-                    const f3 a = ld3(vtx + 3ull * idx[prim + 0]);
-                    const f3 bb = ld3(vtx + 3ull * idx[prim + 1]);
-                    const f3 c = ld3(vtx + 3ull * idx[prim + 2]);
-                    h.normal = normalize(cross(bb - a, c - a));
-                }
-                h.front = dot(ps.ray.direction, h.normal) < 0.0f;
-                if (!h.front) h.normal = h.normal * -1.0f;
-                if (COUNT) cnt.hits++;
-            }
-            h.p = ps.ray.origin + h.t * ps.ray.direction; /* :205 */
+            const Hit h = resolve_hit(ps.ray, hi.x, prim, __float_as_uint(hi.z), spheres, draws);
+            if (COUNT && h.hit) cnt.hits++;
             f3 L;
             if (!path_shade(ps, h, seed, sd, mats, L)) {
                 cont = true;

@@ -71,7 +71,7 @@ struct wcpt_context {
     uint32_t* d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
-    int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + scratch spill */
+    int stack_kind = 0;                /* WCPT_OPTION_STACK: 0 scratch (default; measured faster on c2), 1 LDS + spill */
     int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
