@@ -63,6 +63,12 @@ extern "C" {
 #define WCPT_OPTION_DIAGNOSTICS 2  /* 1: wcpt_render_counters also fills the SIMD-efficiency fields      */
 #define WCPT_OPTION_SORT_RAYS   3  /* wavefront: sort bounce rays by (octant, origin Morton) (default 0) */
 #define WCPT_OPTION_WF_STACK    4  /* wavefront: LDS traversal-stack entries per lane, 10 | 16 | 24 (default 10) */
+/* Derived triangle records. wcpt_render derives per draw command one 48-byte record per triangle (a, b-a, c-a)
+ * from the draw's index and vertex buffers; leaf tests read them instead of index + vertex gathers (same
+ * arithmetic, same results). 1 (default): rebuilt only when a draw's buffers were re-uploaded through
+ * wcpt_buffer_upload / re-allocated, or its buffers or index count changed. 0: rebuilt on every render (use this
+ * when the application writes vertex/index buffers by other means, e.g. its own kernels). */
+#define WCPT_OPTION_TRIANGLE_CACHE 5
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

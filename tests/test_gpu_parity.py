@@ -262,3 +262,81 @@ def test_golden_fixtures(gpu_ctx):
             acc = img
         ref = gold[key]
         assert_close(acc[..., :3].copy(), ref)
+
+
+# ---- derived triangle records (wcpt.h WCPT_OPTION_TRIANGLE_CACHE) -------------------------------------------
+def _with_mesh(s, mesh):
+    import copy
+    d = copy.copy(s)
+    d.meshes = [mesh]
+    return d
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("cache", [1, 0])
+def test_triangle_records_follow_reuploads(gpu_ctx, kernel, cache):
+    """Re-uploading the vertex buffer must re-derive the records: the second frame renders the moved geometry
+    (the BVH is left as it was, which the oracle traverses identically)."""
+    s = get_scene("cornell")
+    W, H = 64, 48
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    gpu_ctx.set_kernel(kernel)
+    gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, cache)
+    try:
+        gpu_ctx.create_screen(W, H)
+        sd = s.scene_data(W, H, max_bounce=3)
+        for step in range(3):
+            m = s.meshes[0]
+            pos = m.positions + np.float32(0.05 * step)
+            gpu_ctx.buffer_upload(dev.buffers[2], np.ascontiguousarray(pos, dtype=np.float32))
+            gpu_ctx.render(sd, *dev.addresses())
+            gpu_ctx.sync()
+            img = gpu_ctx.readback(H)
+            moved = _with_mesh(s, wscene.HostBVH(np.ascontiguousarray(pos, dtype=np.float32), m.indices, m.nodes))
+            ref, _ = oracle.render_scene(moved, W, H, max_bounce=3, threads=8)
+            assert_close(img, ref)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 1)
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        dev.free()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_leaf_not_on_triangle_boundary(gpu_ctx, kernel):
+    """A hand-made BVH whose leaves start at index positions that are not multiples of 3, and a draw whose
+    indexCount covers fewer triangles than the leaves reference: both take the index path and must still
+    equal the oracle (the reference kernel reads indices[first + i .. + 2] whatever `first` is)."""
+    rng = np.random.default_rng(7)
+    ntri = 40
+    pos = (rng.random((ntri * 3, 3), dtype=np.float32) * 2.0 - 1.0).astype(np.float32)
+    pos[:, 2] -= 3.0
+    idx = np.arange(ntri * 3 + 2, dtype=np.uint32) % (ntri * 3)
+    lo, hi = pos.min(axis=0), pos.max(axis=0)
+    nodes = np.zeros(3, dtype=wcpt._lib.NODE_DTYPE)
+    nodes[0] = (lo, hi, 1, 0)                         # interior: children 1, 2
+    nodes[1] = (lo, hi, 1, 60)                        # leaf starting at index position 1 (not a multiple of 3)
+    nodes[2] = (lo, hi, 63, 3 * ntri - 63)            # leaf starting at 63 (aligned), beyond indexCount below
+    s = get_scene("default")
+    mesh = wscene.HostBVH(pos, idx, nodes)
+    scene = _with_mesh(s, mesh)
+    W, H = 48, 40
+    dev = wcpt.DeviceScene(gpu_ctx, scene)
+    try:
+        draws = np.zeros(1, dtype=wcpt._lib.DRAW_COMMAND_DTYPE)
+        draws[0] = (gpu_ctx.buffer_address(dev.buffers[2]), gpu_ctx.buffer_address(dev.buffers[3]),
+                    gpu_ctx.buffer_address(dev.buffers[4]), 30, 0)   # indexCount: only 10 triangles
+        gpu_ctx.buffer_upload(dev.buffers[5], draws)
+        gpu_ctx.set_kernel(kernel)
+        gpu_ctx.create_screen(W, H)
+        sd = scene.scene_data(W, H, max_bounce=2)
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()
+        img = gpu_ctx.readback(H)
+        cnt = gpu_ctx.render_counters(sd, *dev.addresses())
+        ref, rcnt = oracle.render_scene(scene, W, H, max_bounce=2, threads=8)
+        assert_close(img, ref)
+        assert cnt == rcnt
+        assert rcnt["triangle_tests"] > 0 and rcnt["hits"] > 0
+    finally:
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        dev.free()

@@ -164,10 +164,9 @@ __device__ __forceinline__ float raySphereNear(const Ray& r, f3 position, float 
 }
 
 /* pathTracer.comp:121-133; returns t or -1 */
-__device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c)
+/* pathTracer.comp:121-133 with the two edges given: e1 = b - a, e2 = c - a (:122-123) */
+__device__ __forceinline__ float rayTriangleE(const Ray& r, f3 a, f3 edgeAB, f3 edgeAC)
 {
-    const f3 edgeAB = b - a;
-    const f3 edgeAC = c - a;
     const f3 oa = r.origin - a;
     const f3 crossRDE2 = cross(r.direction, edgeAC);
     const float inv = 1.0f / dot(edgeAB, crossRDE2);
@@ -176,6 +175,47 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c)
     const float v = dot(r.direction, crossROAE1 * inv);
     const float t = dot(edgeAC, crossROAE1) * inv;
     return (t > 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f) ? t : -1.0f;
+}
+__device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { return rayTriangleE(r, a, b - a, c - a); }
+
+/* Derived triangle records. For each draw command the runtime derives, from the draw's index and vertex buffers,
+ * one 48-byte record per triangle k (index positions 3k..3k+2): (a.xyz, e1.x) (e1.yz, e2.xy) (e2.z, 0, 0, 0),
+ * with e1 = b - a and e2 = c - a computed by the same binary32 subtractions as :122-123. A leaf test then is
+ * three aligned 16-byte loads instead of an index fetch followed by three dependent vertex gathers, and the
+ * 6 edge subtractions leave the inner loop. The reference's BVH keeps each leaf's index triples contiguous
+ * (PathTracingRenderer.jai:233), so a leaf's records are contiguous too. A leaf whose first index position is
+ * not a multiple of 3 (never produced by the reference's builder) reads the index path. */
+typedef const WCPT_GLOBAL v4f* gtri_ptr;
+struct TriE { f3 a, e1, e2; };
+__device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
+{
+    const gtri_ptr q = t + 3ull * k;
+    const v4f r0 = q[0], r1 = q[1], r2 = q[2];
+    TriE e;
+    e.a = mk3(r0.x, r0.y, r0.z);
+    e.e1 = mk3(r0.w, r1.x, r1.y);
+    e.e2 = mk3(r1.z, r1.w, r2.x);
+    return e;
+}
+__device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
+{
+    const f3 a = ld3(vtx + 3ull * idx[first + 0]);
+    const f3 b = ld3(vtx + 3ull * idx[first + 1]);
+    const f3 c = ld3(vtx + 3ull * idx[first + 2]);
+    TriE e;
+    e.a = a;
+    e.e1 = b - a;
+    e.e2 = c - a;
+    return e;
+}
+/* Leaf cursor into the records: record index of the leaf's first triangle, or kNoRecord for a leaf that does not
+ * start on a triangle boundary or is not fully covered by the draw's `ntri` records. The per-draw table entry
+ * is {record address, ntri} (2 x u64). */
+constexpr uint32_t kNoRecord = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t leaf_record(uint32_t first, uint32_t count, uint32_t ntri)
+{
+    const uint32_t k = first / 3u;
+    return (k * 3u == first && (uint64_t)k + (count + 2u) / 3u <= ntri) ? k : kNoRecord;
 }
 
 /* Per-lane work counters; reduced per wave and added to global u64 counters. */
@@ -307,7 +347,8 @@ __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t pri
 /* pathTracer.comp:135-211 */
 template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
-                                         const wcpt_draw_command* __restrict__ draws, Stack& stk,
+                                         const wcpt_draw_command* __restrict__ draws,
+                                         const uint64_t* __restrict__ tri_records, Stack& stk,
                                          Counters& cnt, bool& overflow)
 {
     float rt = kInfinity;
@@ -332,6 +373,8 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         const gnode_ptr bvh = as_nodes(draws[i].bvhBuffer);
         const gu32_ptr indices = as_u32(draws[i].indexBuffer);
         const gf32_ptr vertices = as_f32(draws[i].vertexBuffer);
+        const gtri_ptr tris = (gtri_ptr)(uintptr_t)tri_records[2u * i];
+        const uint32_t ntri = (uint32_t)tri_records[2u * i + 1u];
         if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
 
         /* root: pushed untested, popped and tested (:155-162) */
@@ -344,15 +387,11 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         for (;;) {
             if (curCount > 0) {
                 /* leaf (:164-178) */
-                for (uint32_t k = 0; k < curCount; k += 3) {
+                const uint32_t rec0 = leaf_record(curLeft, curCount, ntri);
+                for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
                     const uint32_t first = k + curLeft;
-                    const uint32_t ia = indices[first + 0];
-                    const uint32_t ib = indices[first + 1];
-                    const uint32_t ic = indices[first + 2];
-                    const f3 a = ld3(vertices + 3ull * ia);
-                    const f3 b = ld3(vertices + 3ull * ib);
-                    const f3 c = ld3(vertices + 3ull * ic);
-                    const float t = rayTriangle(ray, a, b, c);
+                    const TriE tr = rec0 != kNoRecord ? load_tri(tris, rec0 + j) : tri_from_indices(indices, vertices, first);
+                    const float t = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
                     if (COUNT) {
                         cnt.triangle_tests++;
                         simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
@@ -513,14 +552,15 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
 template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_data& sd,
                                        const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
-                                       const wcpt_draw_command* __restrict__ draws, Stack& stk,
+                                       const wcpt_draw_command* __restrict__ draws,
+                                       const uint64_t* __restrict__ tri_records, Stack& stk,
                                        Counters& cnt, bool& overflow)
 {
     PathState ps;
     path_begin(ps, ray.origin, ray.direction);
     f3 L;
     for (;;) {
-        const Hit h = intersect<COUNT, DIAG>(ps.ray, sd, spheres, draws, stk, cnt, overflow);
+        const Hit h = intersect<COUNT, DIAG>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
         if (path_shade(ps, h, rng, sd, mats, L)) return L;
     }
 }

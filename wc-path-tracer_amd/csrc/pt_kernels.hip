@@ -33,7 +33,8 @@ __device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTot
 template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcpt_material* __restrict__ mats,
                                             const wcpt_sphere* __restrict__ spheres,
-                                            const wcpt_draw_command* __restrict__ draws, float4* __restrict__ image,
+                                            const wcpt_draw_command* __restrict__ draws,
+                                            const uint64_t* __restrict__ tri_records, float4* __restrict__ image,
                                             uint32_t W, uint32_t H, uint32_t y0, uint32_t lx, uint32_t ly, Stack& stk,
                                             Counters& cnt, bool& overflow)
 {
@@ -48,7 +49,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
         r.origin = origin;
         r.direction = dir;
         r.invDirection = rcp3(dir);
-        result = result + TraceRay<COUNT, DIAG>(r, seed, sd, mats, spheres, draws, stk, cnt, overflow);
+        result = result + TraceRay<COUNT, DIAG>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow);
     }
     result = result / (float)sd.samples; /* :312 */
     if (!COUNT) {
@@ -73,6 +74,7 @@ template <bool COUNT, bool DIAG, int SK>
 __global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                     const wcpt_sphere* __restrict__ spheres,
                                                     const wcpt_draw_command* __restrict__ draws,
+                                                    const uint64_t* __restrict__ tri_records,
                                                     float4* __restrict__ image, uint32_t W, uint32_t H, uint32_t y0,
                                                     uint32_t rows, uint32_t tilesX, uint32_t tilesTotal,
                                                     uint32_t* __restrict__ status,
@@ -89,18 +91,32 @@ __global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, co
             uint64_t mem[kPrivateStack];
             PrivateStack<kPrivateStack> stk;
             stk.mem = (priv_u64_ptr)mem;
-            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, image, W, H, y0, lx, ly, stk, cnt, overflow);
+            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, tri_records, image, W, H, y0, lx, ly, stk, cnt, overflow);
         } else {
             __shared__ uint64_t s_stack[kLdsStack * 64];
             uint64_t spill[kSpillStack];
             LdsStack<kLdsStack, kSpillStack> stk;
             stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
             stk.spill = (priv_u64_ptr)spill;
-            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, image, W, H, y0, lx, ly, stk, cnt, overflow);
+            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, tri_records, image, W, H, y0, lx, ly, stk, cnt, overflow);
         }
     }
     if (overflow) atomicOr(status, 1u);
     flush_counters<COUNT>(cnt, counters);
+}
+
+/* Derived triangle records: one thread per triangle. Same subtractions as rayTriangle (:122-123). */
+__global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restrict__ idx, const float* __restrict__ vtx,
+                                                         uint32_t ntri, float4* __restrict__ out)
+{
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= ntri) return;
+    const uint32_t ia = idx[3ull * k + 0], ib = idx[3ull * k + 1], ic = idx[3ull * k + 2];
+    const f3 a = ld3(vtx + 3ull * ia), b = ld3(vtx + 3ull * ib), c = ld3(vtx + 3ull * ic);
+    const f3 e1 = b - a, e2 = c - a;
+    out[3ull * k + 0] = make_float4(a.x, a.y, a.z, e1.x);
+    out[3ull * k + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    out[3ull * k + 2] = make_float4(e2.z, 0.0f, 0.0f, 0.0f);
 }
 
 /* Device self-tests: evaluate the device definitions of the RNG and the deterministic libm on host inputs. */
@@ -137,11 +153,20 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
 } // namespace dev
 
 /* ------------------------------------------------------------------------------------------------ */
+hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* out,
+                                    hipStream_t stream)
+{
+    if (triangles == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::build_tri_records, dim3((triangles + 255u) / 256u), dim3(256), 0, stream, indices, vertices,
+                       triangles, static_cast<float4*>(out));
+    return hipGetLastError();
+}
+
 template <bool COUNT, bool DIAG, int SK>
 static void launch_mega(const LaunchArgs& a, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
 {
     hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK>), dim3(tiles), dim3(64), 0, stream, a.sd, a.materials,
-                       a.spheres, a.draws, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
+                       a.spheres, a.draws, a.tri_records, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
 }
 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream)

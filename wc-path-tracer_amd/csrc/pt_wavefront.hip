@@ -149,14 +149,19 @@ constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
 
 struct Geom {
+    gtri_ptr tris;
+    uint32_t ntri;
     gnode_ptr bvh;
     gu32_ptr indices;
     gf32_ptr vertices;
 };
 
-__device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ draws, uint32_t d)
+__device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ draws,
+                                          const uint64_t* __restrict__ tri_records, uint32_t d)
 {
     Geom g;
+    g.tris = (gtri_ptr)(uintptr_t)tri_records[2u * d];
+    g.ntri = (uint32_t)tri_records[2u * d + 1u];
     g.bvh = as_nodes(draws[d].bvhBuffer);
     g.indices = as_u32(draws[d].indexBuffer);
     g.vertices = as_f32(draws[d].vertexBuffer);
@@ -177,17 +182,21 @@ __device__ __forceinline__ void diag_mark(uint64_t* tim, uint64_t& tprev, int k)
     if (k == 0) tim[6] += 1;
 }
 
-/* Node cursor: interior -> (a = left child index); leaf -> (a = current index position, b = end position). */
-__device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, uint32_t& a, uint32_t& b, uint32_t& mode)
+/* Node cursor: interior -> (a = left child index); leaf -> (a = current index position, b = end position,
+ * r = record of the current triangle or kNoRecord). */
+__device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, uint32_t ntri, uint32_t& a, uint32_t& b,
+                                            uint32_t& r, uint32_t& mode)
 {
     a = left;
     b = left + count;
+    r = leaf_record(left, count, ntri);
     mode = count > 0 ? kModeLeaf : kModeInterior;
 }
 
 template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
 __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
-                                                  const wcpt_draw_command* __restrict__ draws, WfBuffers b,
+                                                  const wcpt_draw_command* __restrict__ draws,
+                                                  const uint64_t* __restrict__ tri_records, WfBuffers b,
                                                   uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
 {
     __shared__ uint64_t s_stack[LDSN * 64];
@@ -201,13 +210,13 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     stk.sp = 0;
     Counters cnt = {};
     bool overflow = false;
-    Geom g0 = {nullptr, nullptr, nullptr}, gl = {nullptr, nullptr, nullptr};
-    if (SINGLE) g0 = load_geom(draws, 0); /* kernel-uniform: scalar registers */
+    Geom g0 = {nullptr, 0u, nullptr, nullptr, nullptr}, gl = {nullptr, 0u, nullptr, nullptr, nullptr};
+    if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
 
     bool has = false, drained = false;
     uint32_t lo = 0, hi = 0; /* this wave's claimed queue range [lo, hi) (wave-uniform) */
     uint32_t p = 0, d = 0, prim = kNoPrim, primDraw = 0;
-    uint32_t ca = 0, cb = 0, mode = kModeDone;
+    uint32_t ca = 0, cb = 0, cr = 0, mode = kModeDone;
     float rt = kInfinity;
     Ray ray;
     uint64_t tim[kDiagTimers] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -216,14 +225,14 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     /* Start draw command d, or the next one whose root survives the cull (:152-162); kModeDone past the last. */
     auto start_draw = [&]() {
         for (; d < sd.drawCommandCount; d++) {
-            if (!SINGLE) gl = load_geom(draws, d);
+            if (!SINGLE) gl = load_geom(draws, tri_records, d);
             const Geom& g = SINGLE ? g0 : gl;
             if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
             const NodeV root = load_node(g.bvh, 0);
             float c0, c1;
             node_box(ray, root, c0, c1);
             if (c0 > c1 || c1 < 0.0f || c0 > rt) continue;
-            cursor_from(root.b.z, root.b.w, ca, cb, mode);
+            cursor_from(root.b.z, root.b.w, g.ntri, ca, cb, cr, mode);
             stk.reset();
             return;
         }
@@ -274,11 +283,8 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             /* one traversal step (:157-200); the phases are sequential ifs (a lane's mode changes only
              * LEAF->POP or INTERIOR->{LEAF,INTERIOR,POP} in a step, so this equals if / else if) */
             if (has && mode == kModeLeaf) {
-                const uint32_t ia = g.indices[ca + 0];
-                const uint32_t ib = g.indices[ca + 1];
-                const uint32_t ic = g.indices[ca + 2];
-                const float tt = rayTriangle(ray, ld3(g.vertices + 3ull * ia), ld3(g.vertices + 3ull * ib),
-                                             ld3(g.vertices + 3ull * ic));
+                const TriE tr = cr != kNoRecord ? load_tri(g.tris, cr) : tri_from_indices(g.indices, g.vertices, ca);
+                const float tt = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
                 if (COUNT) {
                     cnt.triangle_tests++;
                     simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
@@ -289,6 +295,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     primDraw = d;
                 }
                 ca += 3;
+                cr += (cr != kNoRecord) ? 1u : 0u;
                 if (ca >= cb) mode = kModePop;
             }
             diag_mark<DIAG>(tim, tprev, 1);
@@ -313,7 +320,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 if (passFar && !stk.push(leftFirst ? ca + 1 : ca, leftFirst ? r0 : l0)) overflow = true;
                 if (passNear && !((leftFirst ? l0 : r0) > rt)) {
                     const uint32_t nl = leftFirst ? L.b.z : R.b.z, nc = leftFirst ? L.b.w : R.b.w;
-                    cursor_from(nl, nc, ca, cb, mode);
+                    cursor_from(nl, nc, g.ntri, ca, cb, cr, mode);
                 } else {
                     mode = kModePop;
                 }
@@ -327,7 +334,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     stk.pop(ni, t0);
                     if (t0 > rt) continue;
                     const uint2 lc = load_node_lc(g.bvh, ni);
-                    cursor_from(lc.x, lc.y, ca, cb, mode);
+                    cursor_from(lc.x, lc.y, g.ntri, ca, cb, cr, mode);
                     found = true;
                     break;
                 }
@@ -538,7 +545,7 @@ static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace
                          hipStream_t stream)
 {
     hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
-                       b, a.status, a.counters);
+                       a.tri_records, b, a.status, a.counters);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
                        a.spheres, a.draws, b, a.image, a.W, a.H, a.y0, a.counters);
 }

@@ -37,6 +37,23 @@ struct Buffer {
     void* raw = nullptr;   /* hipMalloc result */
     void* ptr = nullptr;   /* raw + kBufferSkew: the device address handed out */
     uint64_t bytes = 0;
+    uint64_t generation = 0;      /* context-wide counter value of the last alloc / upload / grow */
+    std::vector<uint8_t> shadow;  /* host copy of the uploaded contents (buffers <= kShadowMax bytes) */
+};
+
+/* Small buffers (draw commands, materials, spheres) keep a host copy of what was uploaded, so that the render
+ * call can read the draw commands without a device round trip. */
+constexpr uint64_t kShadowMax = 1ull << 20;
+
+/* Derived triangle records of one draw command (pt_device.h): rebuilt when the draw's vertex/index buffers,
+ * their generations or its index count change (or on every render with WCPT_OPTION_TRIANGLE_CACHE = 0). */
+constexpr uint64_t kUnknownGeneration = ~0ull;
+struct TriRecords {
+    uint64_t vb = 0, ib = 0, gen_vb = kUnknownGeneration, gen_ib = kUnknownGeneration;
+    uint32_t ntri = 0;
+    bool valid = false;
+    void* mem = nullptr;
+    uint64_t cap = 0;
 };
 
 hipError_t skewed_alloc(Buffer& b, uint64_t bytes)
@@ -75,6 +92,12 @@ struct wcpt_context {
     int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
+    int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
+    uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
+    std::vector<TriRecords> tri;       /* per draw command index */
+    std::vector<uint64_t> tri_table;   /* host image of d_tri_table: {address, ntri} per draw */
+    uint64_t* d_tri_table = nullptr;
+    uint32_t tri_table_cap = 0;        /* draws d_tri_table can hold */
     std::string last_error;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -155,6 +178,100 @@ int alloc_image(wcpt_context* ctx, uint32_t w, uint32_t h, uint32_t y0, uint32_t
     return WCPT_SUCCESS;
 }
 
+/* The buffer whose [ptr, ptr + bytes) contains device address `addr`, or null. */
+Buffer* buffer_at(wcpt_context* ctx, uint64_t addr, uint64_t& offset)
+{
+    for (auto& kv : ctx->buffers) {
+        const uint64_t base = reinterpret_cast<uint64_t>(kv.second.ptr);
+        if (kv.second.ptr && addr >= base && addr < base + kv.second.bytes) {
+            offset = addr - base;
+            return &kv.second;
+        }
+    }
+    return nullptr;
+}
+
+/* Derive (or reuse) the triangle records of every draw command and point a.tri_records at the table. The
+ * draw commands are read from the host copy of their buffer when the context owns it, else from the device. */
+int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t draws, wcpt::LaunchArgs& a)
+{
+    const uint32_t n = sd.drawCommandCount;
+    a.tri_records = nullptr;
+    if (n == 0) return WCPT_SUCCESS;
+    std::vector<wcpt_draw_command> dc(n);
+    const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
+    uint64_t off = 0;
+    Buffer* db = buffer_at(ctx, draws, off);
+    if (db && off + dbytes <= db->shadow.size()) {
+        std::memcpy(dc.data(), db->shadow.data() + off, dbytes);
+    } else {
+        HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
+                                    ctx->stream), "hipMemcpyAsync(draw commands)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
+    }
+    if (ctx->tri.size() < n) ctx->tri.resize(n);
+    bool table_dirty = ctx->tri_table.size() < 2ull * n;
+    if (table_dirty) ctx->tri_table.resize(2ull * n, 0);
+    for (uint32_t d = 0; d < n; d++) {
+        TriRecords& t = ctx->tri[d];
+        const uint64_t vb = dc[d].vertexBuffer, ib = dc[d].indexBuffer;
+        uint64_t o = 0;
+        Buffer* bv = buffer_at(ctx, vb, o);
+        Buffer* bi = buffer_at(ctx, ib, o);
+        const uint64_t gv = bv ? bv->generation : kUnknownGeneration;
+        const uint64_t gi = bi ? bi->generation : kUnknownGeneration;
+        const uint32_t ntri = dc[d].indexCount / 3u;
+        const bool reuse = ctx->tri_cache && t.valid && t.vb == vb && t.ib == ib && t.ntri == ntri && t.gen_vb == gv &&
+                           t.gen_ib == gi && gv != kUnknownGeneration && gi != kUnknownGeneration;
+        if (!reuse) {
+            const uint64_t bytes = (uint64_t)(ntri ? ntri : 1u) * wcpt::kTriRecordBytes;
+            if (t.cap < bytes) {
+                if (t.mem) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+                if (t.mem) (void)hipFree(t.mem);
+                t.mem = nullptr;
+                t.cap = 0;
+                HIP_TRY(ctx, hipMalloc(&t.mem, bytes), "hipMalloc(triangle records)");
+                t.cap = bytes;
+            }
+            if (ntri && (vb == 0 || ib == 0))
+                return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "draw command %u: null vertex/index buffer", d);
+            HIP_TRY(ctx, wcpt::launch_build_tri_records(reinterpret_cast<const uint32_t*>(ib),
+                                                        reinterpret_cast<const float*>(vb), ntri, t.mem, ctx->stream),
+                    "build_tri_records");
+            t.vb = vb;
+            t.ib = ib;
+            t.gen_vb = gv;
+            t.gen_ib = gi;
+            t.ntri = ntri;
+            t.valid = true;
+        }
+        const uint64_t addr = reinterpret_cast<uint64_t>(t.mem);
+        if (ctx->tri_table[2ull * d] != addr || ctx->tri_table[2ull * d + 1] != ntri) {
+            ctx->tri_table[2ull * d] = addr;
+            ctx->tri_table[2ull * d + 1] = ntri;
+            table_dirty = true;
+        }
+    }
+    if (ctx->tri_table_cap < n) {
+        if (ctx->d_tri_table) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+            (void)hipFree(ctx->d_tri_table);
+        }
+        ctx->d_tri_table = nullptr;
+        ctx->tri_table_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&ctx->d_tri_table, 2ull * n * sizeof(uint64_t)), "hipMalloc(triangle record table)");
+        ctx->tri_table_cap = n;
+        table_dirty = true;
+    }
+    if (table_dirty) {
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_tri_table, ctx->tri_table.data(), 2ull * n * sizeof(uint64_t),
+                                    hipMemcpyHostToDevice, ctx->stream), "hipMemcpyAsync(triangle record table)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(triangle record table)");
+    }
+    a.tri_records = ctx->d_tri_table;
+    return WCPT_SUCCESS;
+}
+
 int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                   uint64_t draws, int mode)
 {
@@ -181,6 +298,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.rows = ctx->rows;
     a.status = ctx->d_status;
     a.counters = ctx->d_counters;
+    a.tri_records = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ctx->profiling && mode == wcpt::kModeRender) {
         if (ctx->events_used == ctx->events.size()) {
@@ -194,6 +312,8 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
         ctx->events_used++;
         HIP_TRY(ctx, hipEventRecord(e0, ctx->stream), "hipEventRecord");
     }
+    rc = prepare_tri_records(ctx, *scene, draws, a);
+    if (rc) return rc;
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
     case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->stream); break;
@@ -287,6 +407,9 @@ int wcpt_destroy(wcpt_context* ctx)
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     wcpt::wf_release(ctx->wf);
+    for (auto& t : ctx->tri)
+        if (t.mem) (void)hipFree(t.mem);
+    if (ctx->d_tri_table) (void)hipFree(ctx->d_tri_table);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     for (auto& p : ctx->events) {
         (void)hipEventDestroy(p.first);
@@ -322,6 +445,9 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
         return WCPT_SUCCESS;
+    case WCPT_OPTION_TRIANGLE_CACHE:
+        ctx->tri_cache = value ? 1 : 0;
+        return WCPT_SUCCESS;
     case WCPT_OPTION_WF_STACK:
         if (value != 10 && value != 16 && value != 24)
             return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wavefront LDS stack %d (10, 16 or 24)", value);
@@ -346,6 +472,8 @@ int wcpt_buffer_alloc(wcpt_context* ctx, uint64_t bytes, wcpt_buffer* out)
     if (!out) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null out handle");
     Buffer b;
     HIP_TRY(ctx, skewed_alloc(b, bytes), "hipMalloc(buffer)");
+    b.generation = ++ctx->generation;
+    if (bytes <= kShadowMax) b.shadow.assign(bytes, 0); /* hipMalloc contents are undefined; see upload */
     const uint64_t h = ctx->next_handle++;
     ctx->buffers[h] = b;
     *out = h;
@@ -372,13 +500,18 @@ int wcpt_buffer_upload(wcpt_context* ctx, wcpt_buffer buf, const void* src, uint
             }
         }
         if (b->raw) (void)hipFree(b->raw);
-        *b = nb;
+        nb.shadow = std::move(b->shadow);
+        *b = std::move(nb);
+        if (b->bytes <= kShadowMax) b->shadow.resize(b->bytes, 0);
+        else b->shadow.clear();
     }
     if (bytes) {
         HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(b->ptr) + offset, src, bytes, hipMemcpyHostToDevice, ctx->stream),
                 "hipMemcpyAsync(upload)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(upload)"); /* blocking, like :98-112 */
+        if (b->shadow.size() == b->bytes && b->bytes) std::memcpy(b->shadow.data() + offset, src, bytes);
     }
+    b->generation = ++ctx->generation;
     return WCPT_SUCCESS;
 }
 

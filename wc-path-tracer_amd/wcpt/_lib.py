@@ -42,6 +42,7 @@ OPTION_STACK = 1
 OPTION_DIAGNOSTICS = 2
 OPTION_SORT_RAYS = 3
 OPTION_WF_STACK = 4
+OPTION_TRIANGLE_CACHE = 5
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
