@@ -69,6 +69,9 @@ extern "C" {
  * wcpt_buffer_upload / re-allocated, or its buffers or index count changed. 0: rebuilt on every render (use this
  * when the application writes vertex/index buffers by other means, e.g. its own kernels). */
 #define WCPT_OPTION_TRIANGLE_CACHE 5
+/* Megakernel leaf tests: -1 (default) choose by mean triangles per leaf; 0 single records; 1 pair records
+ * (two triangles per lane with packed-FP32 arithmetic). Results are identical either way. */
+#define WCPT_OPTION_PAIR_RECORDS 6
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

@@ -340,3 +340,18 @@ def test_leaf_not_on_triangle_boundary(gpu_ctx, kernel):
     finally:
         gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
         dev.free()
+
+
+@pytest.mark.parametrize("pairs", [0, 1])
+@pytest.mark.parametrize("name,W,H", [("cornell", 80, 64), ("atrium", 64, 40), ("default", 48, 40)])
+def test_record_formats_match_oracle(gpu_ctx, pairs, name, W, H):
+    """Megakernel leaf tests on single records and on packed pair records: both equal the oracle."""
+    s = get_scene(name)
+    gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, pairs)
+    try:
+        img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=3)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, -1)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=3, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt

@@ -178,13 +178,23 @@ __device__ __forceinline__ float rayTriangleE(const Ray& r, f3 a, f3 edgeAB, f3 
 }
 __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { return rayTriangleE(r, a, b - a, c - a); }
 
-/* Derived triangle records. For each draw command the runtime derives, from the draw's index and vertex buffers,
- * one 48-byte record per triangle k (index positions 3k..3k+2): (a.xyz, e1.x) (e1.yz, e2.xy) (e2.z, 0, 0, 0),
- * with e1 = b - a and e2 = c - a computed by the same binary32 subtractions as :122-123. A leaf test then is
- * three aligned 16-byte loads instead of an index fetch followed by three dependent vertex gathers, and the
- * 6 edge subtractions leave the inner loop. The reference's BVH keeps each leaf's index triples contiguous
- * (PathTracingRenderer.jai:233), so a leaf's records are contiguous too. A leaf whose first index position is
- * not a multiple of 3 (never produced by the reference's builder) reads the index path. */
+/* Derived triangle records. For each draw command the runtime derives from the draw's index and vertex buffers,
+ * triangle k = index positions 3k..3k+2, with e1 = b - a and e2 = c - a computed by the same binary32
+ * subtractions as :122-123, two record arrays:
+ *   single records, 48 B per triangle: (a.xyz, e1.x) (e1.yz, e2.xy) (e2.z, 0, 0, 0);
+ *   pair records, 80 B per triangle pair (2j, 2j+1): the nine components of both triangles as float2
+ *     {tri 2j, tri 2j+1} + 8 B pad. One lane then tests two triangles at once with packed-FP32 instructions
+ *     (v_pk_mul_f32 / v_pk_add_f32 perform two independent binary32 ops each -- exactly the reference's ops),
+ *     halving the VALU issue slots of the Möller-Trumbore arithmetic; the two results are applied in
+ *     reference order (2j first, then 2j+1, strict <).
+ * A leaf test reads aligned 16-byte loads instead of an index fetch plus three dependent vertex gathers, and
+ * the edge subtractions leave the inner loop. Pairs pay off for fat leaves (the Cornell box: ~17 triangles per
+ * leaf, VALU-bound); single records for thin leaves (the atrium: ~2 triangles per leaf, fetch-latency-bound).
+ * The reference's BVH keeps each leaf's index triples contiguous (PathTracingRenderer.jai:233), so a leaf's
+ * records are contiguous. A leaf whose first index position is not a multiple of 3 (never produced by the
+ * reference's builder) or that reaches past the draw's indexCount uses the index path.
+ * Per-draw table entry: {single record address, pair record address, triangle count, -} (4 x u64). */
+constexpr uint32_t kTriTableWords = 4;
 typedef const WCPT_GLOBAL v4f* gtri_ptr;
 struct TriE { f3 a, e1, e2; };
 __device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
@@ -197,6 +207,48 @@ __device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
     e.e2 = mk3(r1.z, r1.w, r2.x);
     return e;
 }
+typedef float v2f __attribute__((ext_vector_type(2)));
+constexpr uint32_t kPairRecordFloat4s = 5;
+struct TriPair { v2f ax, ay, az, e1x, e1y, e1z, e2x, e2y, e2z; };
+__device__ __forceinline__ TriPair load_pair(gtri_ptr t, uint32_t j)
+{
+    const gtri_ptr q = t + (uint64_t)kPairRecordFloat4s * j;
+    const v4f r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    TriPair p;
+    p.ax = r0.xy;  p.ay = r0.zw;
+    p.az = r1.xy;  p.e1x = r1.zw;
+    p.e1y = r2.xy; p.e1z = r2.zw;
+    p.e2x = r3.xy; p.e2y = r3.zw;
+    p.e2z = r4.xy;
+    return p;
+}
+__device__ __forceinline__ v2f bc2(float s) { v2f r = {s, s}; return r; }
+/* rayTriangleE for the two triangles of a pair; t.x for triangle 2j, t.y for 2j+1 (-1 = miss). */
+__device__ __forceinline__ v2f rayTrianglePair(const Ray& r, const TriPair& p)
+{
+    const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
+    const v2f oax = bc2(r.origin.x) - p.ax, oay = bc2(r.origin.y) - p.ay, oaz = bc2(r.origin.z) - p.az;
+    /* crossRDE2 = cross(d, e2) */
+    const v2f px = dy * p.e2z - p.e2y * dz;
+    const v2f py = dz * p.e2x - p.e2z * dx;
+    const v2f pz = dx * p.e2y - p.e2x * dy;
+    const v2f det = (p.e1x * px + p.e1y * py) + p.e1z * pz;
+    v2f inv;
+    inv.x = 1.0f / det.x;
+    inv.y = 1.0f / det.y;
+    /* crossROAE1 = cross(oa, e1) */
+    const v2f qx = oay * p.e1z - p.e1y * oaz;
+    const v2f qy = oaz * p.e1x - p.e1z * oax;
+    const v2f qz = oax * p.e1y - p.e1x * oay;
+    const v2f u = ((oax * px + oay * py) + oaz * pz) * inv;
+    const v2f v = (dx * (qx * inv) + dy * (qy * inv)) + dz * (qz * inv);
+    const v2f t = ((p.e2x * qx + p.e2y * qy) + p.e2z * qz) * inv;
+    const v2f uv = u + v;
+    v2f res;
+    res.x = (t.x > 0.0f && u.x >= 0.0f && u.x <= 1.0f && v.x >= 0.0f && uv.x <= 1.0f) ? t.x : -1.0f;
+    res.y = (t.y > 0.0f && u.y >= 0.0f && u.y <= 1.0f && v.y >= 0.0f && uv.y <= 1.0f) ? t.y : -1.0f;
+    return res;
+}
 __device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
 {
     const f3 a = ld3(vtx + 3ull * idx[first + 0]);
@@ -208,7 +260,7 @@ __device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uin
     e.e2 = c - a;
     return e;
 }
-/* Leaf cursor into the records: record index of the leaf's first triangle, or kNoRecord for a leaf that does not
+/* Leaf cursor into the records: triangle index of the leaf's first triangle, or kNoRecord for a leaf that does not
  * start on a triangle boundary or is not fully covered by the draw's `ntri` records. The per-draw table entry
  * is {record address, ntri} (2 x u64). */
 constexpr uint32_t kNoRecord = 0xFFFFFFFFu;
@@ -344,8 +396,8 @@ __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t pri
     return h;
 }
 
-/* pathTracer.comp:135-211 */
-template <bool COUNT, bool DIAG, class Stack>
+/* pathTracer.comp:135-211. PAIRS: leaf tests on pair records (else single records). */
+template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
                                          const wcpt_draw_command* __restrict__ draws,
                                          const uint64_t* __restrict__ tri_records, Stack& stk,
@@ -373,8 +425,8 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         const gnode_ptr bvh = as_nodes(draws[i].bvhBuffer);
         const gu32_ptr indices = as_u32(draws[i].indexBuffer);
         const gf32_ptr vertices = as_f32(draws[i].vertexBuffer);
-        const gtri_ptr tris = (gtri_ptr)(uintptr_t)tri_records[2u * i];
-        const uint32_t ntri = (uint32_t)tri_records[2u * i + 1u];
+        const gtri_ptr tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + (PAIRS ? 1u : 0u)];
+        const uint32_t ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
         if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
 
         /* root: pushed untested, popped and tested (:155-162) */
@@ -387,19 +439,49 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         for (;;) {
             if (curCount > 0) {
                 /* leaf (:164-178) */
-                const uint32_t rec0 = leaf_record(curLeft, curCount, ntri);
-                for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
-                    const uint32_t first = k + curLeft;
-                    const TriE tr = rec0 != kNoRecord ? load_tri(tris, rec0 + j) : tri_from_indices(indices, vertices, first);
-                    const float t = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
-                    if (COUNT) {
-                        cnt.triangle_tests++;
-                        simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
+                const uint32_t k0 = leaf_record(curLeft, curCount, ntri);
+                if (PAIRS && k0 != kNoRecord) {
+                    const uint32_t kend = k0 + (curCount + 2u) / 3u;
+                    for (uint32_t k = k0 & ~1u; k < kend; k += 2) {
+                        const v2f tt = rayTrianglePair(ray, load_pair(tris, k >> 1));
+                        if (k >= k0) {
+                            if (COUNT) {
+                                cnt.triangle_tests++;
+                                simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
+                            }
+                            if (tt.x != -1.0f && tt.x < rt) {
+                                rt = tt.x;
+                                prim = 3u * k;
+                                primDraw = i;
+                            }
+                        }
+                        if (k + 1u < kend) {
+                            if (COUNT) {
+                                cnt.triangle_tests++;
+                                simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
+                            }
+                            if (tt.y != -1.0f && tt.y < rt) {
+                                rt = tt.y;
+                                prim = 3u * (k + 1u);
+                                primDraw = i;
+                            }
+                        }
                     }
-                    if (t != -1.0f && t < rt) {
-                        rt = t;
-                        prim = first;
-                        primDraw = i;
+                } else {
+                    for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
+                        const uint32_t first = k + curLeft;
+                        const TriE tr = (!PAIRS && k0 != kNoRecord) ? load_tri(tris, k0 + j)
+                                                                    : tri_from_indices(indices, vertices, first);
+                        const float t = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
+                        if (COUNT) {
+                            cnt.triangle_tests++;
+                            simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
+                        }
+                        if (t != -1.0f && t < rt) {
+                            rt = t;
+                            prim = first;
+                            primDraw = i;
+                        }
                     }
                 }
             } else {
@@ -549,7 +631,7 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
 }
 
 /* pathTracer.comp:241-284 */
-template <bool COUNT, bool DIAG, class Stack>
+template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
 __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_data& sd,
                                        const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
                                        const wcpt_draw_command* __restrict__ draws,
@@ -560,7 +642,7 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
     path_begin(ps, ray.origin, ray.direction);
     f3 L;
     for (;;) {
-        const Hit h = intersect<COUNT, DIAG>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
+        const Hit h = intersect<COUNT, DIAG, PAIRS>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
         if (path_shade(ps, h, rng, sd, mats, L)) return L;
     }
 }

@@ -22,7 +22,8 @@ struct LaunchArgs {
     const wcpt_material* materials;
     const wcpt_sphere* spheres;
     const wcpt_draw_command* draws;
-    const uint64_t* tri_records; /* device table [drawCommandCount] of {record address, triangle count} */
+    const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
+    bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     float4* image;
     uint32_t W, H, y0, rows;
     uint32_t* status;
@@ -65,10 +66,11 @@ struct WfState {
  * diagnostics (ballot-based step counters, tools/diag.py). */
 constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
 
-/* Derived triangle records (pt_device.h): record k = (a, b - a, c - a) of index positions 3k..3k+2. */
-constexpr uint32_t kTriRecordBytes = 48;
-hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* out,
-                                    hipStream_t stream);
+/* Derived triangle records (pt_device.h): triangle k = index positions 3k..3k+2 stored as (a, b - a, c - a);
+ * singles: 48 B per triangle; pairs: 80 B per triangle pair (2j, 2j+1). */
+constexpr uint32_t kSingleRecordBytes = 48, kPairRecordBytes = 80;
+hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* singles,
+                                    void* pairs, hipStream_t stream);
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream);
 /* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
 /* lds_stack: LDS traversal-stack entries per lane of the trace kernel (10, 16 or 24; render mode only). */

@@ -30,7 +30,7 @@ __device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTot
 }
 
 /* Shade one pixel (pathTracer.comp:290-323) with the given traversal stack. */
-template <bool COUNT, bool DIAG, class Stack>
+template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
 __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcpt_material* __restrict__ mats,
                                             const wcpt_sphere* __restrict__ spheres,
                                             const wcpt_draw_command* __restrict__ draws,
@@ -49,7 +49,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
         r.origin = origin;
         r.direction = dir;
         r.invDirection = rcp3(dir);
-        result = result + TraceRay<COUNT, DIAG>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow);
+        result = result + TraceRay<COUNT, DIAG, PAIRS>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow);
     }
     result = result / (float)sd.samples; /* :312 */
     if (!COUNT) {
@@ -70,8 +70,12 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
 
 /* Stack kinds: 0 = private (scratch) stack of kPrivateStack entries; 1 = LDS stack of kLdsStack entries per
  * lane with a kSpillStack-entry private spill. */
-template <bool COUNT, bool DIAG, int SK>
-__global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
+/* Occupancy floor for experiments (tools/ab_build.sh): __launch_bounds__'s minimum waves per SIMD. */
+#ifndef WCPT_MK_WAVES
+#define WCPT_MK_WAVES 1
+#endif
+template <bool COUNT, bool DIAG, int SK, bool PAIRS>
+__global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                     const wcpt_sphere* __restrict__ spheres,
                                                     const wcpt_draw_command* __restrict__ draws,
                                                     const uint64_t* __restrict__ tri_records,
@@ -91,32 +95,51 @@ __global__ __launch_bounds__(64) void pt_megakernel(const wcpt_scene_data sd, co
             uint64_t mem[kPrivateStack];
             PrivateStack<kPrivateStack> stk;
             stk.mem = (priv_u64_ptr)mem;
-            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, tri_records, image, W, H, y0, lx, ly, stk, cnt, overflow);
+            shade_pixel<COUNT, DIAG, PAIRS>(sd, mats, spheres, draws, tri_records, image, W, H, y0, lx, ly, stk, cnt, overflow);
         } else {
             __shared__ uint64_t s_stack[kLdsStack * 64];
             uint64_t spill[kSpillStack];
             LdsStack<kLdsStack, kSpillStack> stk;
             stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
             stk.spill = (priv_u64_ptr)spill;
-            shade_pixel<COUNT, DIAG>(sd, mats, spheres, draws, tri_records, image, W, H, y0, lx, ly, stk, cnt, overflow);
+            shade_pixel<COUNT, DIAG, PAIRS>(sd, mats, spheres, draws, tri_records, image, W, H, y0, lx, ly, stk, cnt, overflow);
         }
     }
     if (overflow) atomicOr(status, 1u);
     flush_counters<COUNT>(cnt, counters);
 }
 
-/* Derived triangle records: one thread per triangle. Same subtractions as rayTriangle (:122-123). */
+/* Derived triangle records (pt_device.h), single and pair formats: one thread per pair. Same subtractions as
+ * rayTriangle (:122-123). The second slot of the last pair of an odd count is zero (never inside a leaf's
+ * range: leaf_record bounds leaves by the triangle count). */
 __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restrict__ idx, const float* __restrict__ vtx,
-                                                         uint32_t ntri, float4* __restrict__ out)
+                                                         uint32_t ntri, float4* __restrict__ singles,
+                                                         float4* __restrict__ out)
 {
-    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
-    if (k >= ntri) return;
-    const uint32_t ia = idx[3ull * k + 0], ib = idx[3ull * k + 1], ic = idx[3ull * k + 2];
-    const f3 a = ld3(vtx + 3ull * ia), b = ld3(vtx + 3ull * ib), c = ld3(vtx + 3ull * ic);
-    const f3 e1 = b - a, e2 = c - a;
-    out[3ull * k + 0] = make_float4(a.x, a.y, a.z, e1.x);
-    out[3ull * k + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
-    out[3ull * k + 2] = make_float4(e2.z, 0.0f, 0.0f, 0.0f);
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if (2ull * j >= ntri) return;
+    float v[2][9];
+    for (uint32_t h = 0; h < 2; h++) {
+        const uint64_t k = 2ull * j + h;
+        if (k >= ntri) {
+            for (int c = 0; c < 9; c++) v[h][c] = 0.0f;
+            continue;
+        }
+        const uint32_t ia = idx[3ull * k + 0], ib = idx[3ull * k + 1], ic = idx[3ull * k + 2];
+        const f3 a = ld3(vtx + 3ull * ia), b = ld3(vtx + 3ull * ib), c = ld3(vtx + 3ull * ic);
+        const f3 e1 = b - a, e2 = c - a;
+        const float f[9] = {a.x, a.y, a.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z};
+        for (int c2 = 0; c2 < 9; c2++) v[h][c2] = f[c2];
+        singles[3ull * k + 0] = make_float4(a.x, a.y, a.z, e1.x);
+        singles[3ull * k + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+        singles[3ull * k + 2] = make_float4(e2.z, 0.0f, 0.0f, 0.0f);
+    }
+    float4* o = out + (uint64_t)kPairRecordFloat4s * j;
+    o[0] = make_float4(v[0][0], v[1][0], v[0][1], v[1][1]);
+    o[1] = make_float4(v[0][2], v[1][2], v[0][3], v[1][3]);
+    o[2] = make_float4(v[0][4], v[1][4], v[0][5], v[1][5]);
+    o[3] = make_float4(v[0][6], v[1][6], v[0][7], v[1][7]);
+    o[4] = make_float4(v[0][8], v[1][8], 0.0f, 0.0f);
 }
 
 /* Device self-tests: evaluate the device definitions of the RNG and the deterministic libm on host inputs. */
@@ -153,20 +176,36 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
 } // namespace dev
 
 /* ------------------------------------------------------------------------------------------------ */
-hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* out,
-                                    hipStream_t stream)
+hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* singles,
+                                    void* pairs, hipStream_t stream)
 {
     if (triangles == 0) return hipSuccess;
-    hipLaunchKernelGGL(dev::build_tri_records, dim3((triangles + 255u) / 256u), dim3(256), 0, stream, indices, vertices,
-                       triangles, static_cast<float4*>(out));
+    const uint32_t npairs = (uint32_t)((triangles + 1ull) / 2ull);
+    hipLaunchKernelGGL(dev::build_tri_records, dim3((npairs + 255u) / 256u), dim3(256), 0, stream, indices, vertices,
+                       triangles, static_cast<float4*>(singles), static_cast<float4*>(pairs));
     return hipGetLastError();
 }
 
-template <bool COUNT, bool DIAG, int SK>
+template <bool COUNT, bool DIAG, int SK, bool PAIRS>
 static void launch_mega(const LaunchArgs& a, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
 {
-    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK>), dim3(tiles), dim3(64), 0, stream, a.sd, a.materials,
+    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS>), dim3(tiles), dim3(64), 0, stream, a.sd, a.materials,
                        a.spheres, a.draws, a.tri_records, a.image, a.W, a.H, a.y0, a.rows, tilesX, tiles, a.status, a.counters);
+}
+
+template <bool PAIRS>
+static void launch_mega_sk(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream, uint32_t tilesX,
+                           uint32_t tiles)
+{
+    if (stack_kind == 0) {
+        if (mode == kModeRender) launch_mega<false, false, 0, PAIRS>(a, stream, tilesX, tiles);
+        else if (mode == kModeCount) launch_mega<true, false, 0, PAIRS>(a, stream, tilesX, tiles);
+        else launch_mega<true, true, 0, PAIRS>(a, stream, tilesX, tiles);
+    } else {
+        if (mode == kModeRender) launch_mega<false, false, 1, PAIRS>(a, stream, tilesX, tiles);
+        else if (mode == kModeCount) launch_mega<true, false, 1, PAIRS>(a, stream, tilesX, tiles);
+        else launch_mega<true, true, 1, PAIRS>(a, stream, tilesX, tiles);
+    }
 }
 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream)
@@ -175,15 +214,10 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipS
     const uint32_t tilesY = (a.rows + 7u) / 8u;
     const uint32_t tiles = tilesX * tilesY;
     if (tiles == 0) return hipSuccess;
-    if (stack_kind == 0) {
-        if (mode == kModeRender) launch_mega<false, false, 0>(a, stream, tilesX, tiles);
-        else if (mode == kModeCount) launch_mega<true, false, 0>(a, stream, tilesX, tiles);
-        else launch_mega<true, true, 0>(a, stream, tilesX, tiles);
-    } else {
-        if (mode == kModeRender) launch_mega<false, false, 1>(a, stream, tilesX, tiles);
-        else if (mode == kModeCount) launch_mega<true, false, 1>(a, stream, tilesX, tiles);
-        else launch_mega<true, true, 1>(a, stream, tilesX, tiles);
-    }
+    if (a.pair_records)
+        launch_mega_sk<true>(a, mode, stack_kind, stream, tilesX, tiles);
+    else
+        launch_mega_sk<false>(a, mode, stack_kind, stream, tilesX, tiles);
     return hipGetLastError();
 }
 

@@ -160,8 +160,8 @@ __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ 
                                           const uint64_t* __restrict__ tri_records, uint32_t d)
 {
     Geom g;
-    g.tris = (gtri_ptr)(uintptr_t)tri_records[2u * d];
-    g.ntri = (uint32_t)tri_records[2u * d + 1u];
+    g.tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * d];      /* single records */
+    g.ntri = (uint32_t)tri_records[kTriTableWords * d + 2u];
     g.bvh = as_nodes(draws[d].bvhBuffer);
     g.indices = as_u32(draws[d].indexBuffer);
     g.vertices = as_f32(draws[d].vertexBuffer);
@@ -283,6 +283,8 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             /* one traversal step (:157-200); the phases are sequential ifs (a lane's mode changes only
              * LEAF->POP or INTERIOR->{LEAF,INTERIOR,POP} in a step, so this equals if / else if) */
             if (has && mode == kModeLeaf) {
+                /* one triangle per step, from the single records (pair records measured slower here: most
+                 * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
                 const TriE tr = cr != kNoRecord ? load_tri(g.tris, cr) : tri_from_indices(g.indices, g.vertices, ca);
                 const float tt = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
                 if (COUNT) {

@@ -52,9 +52,15 @@ struct TriRecords {
     uint64_t vb = 0, ib = 0, gen_vb = kUnknownGeneration, gen_ib = kUnknownGeneration;
     uint32_t ntri = 0;
     bool valid = false;
-    void* mem = nullptr;
+    void* mem = nullptr;    /* single records, then pair records */
     uint64_t cap = 0;
+    uint64_t pair_offset = 0;
 };
+
+/* Pair records (packed two-triangle tests) pay off when leaves are fat: mean triangles per leaf >= this,
+ * estimated as triangles / leaves with leaves = (nodes + 1) / 2 from the BVH buffer's size. Measured: the
+ * Cornell box (17 per leaf) gains, the atrium (~2 per leaf) loses. */
+constexpr double kPairMinTrianglesPerLeaf = 4.0;
 
 hipError_t skewed_alloc(Buffer& b, uint64_t bytes)
 {
@@ -93,6 +99,7 @@ struct wcpt_context {
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
+    int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
     std::vector<TriRecords> tri;       /* per draw command index */
     std::vector<uint64_t> tri_table;   /* host image of d_tri_table: {address, ntri} per draw */
@@ -210,8 +217,10 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
     }
     if (ctx->tri.size() < n) ctx->tri.resize(n);
-    bool table_dirty = ctx->tri_table.size() < 2ull * n;
-    if (table_dirty) ctx->tri_table.resize(2ull * n, 0);
+    constexpr uint64_t W = 4; /* table words per draw (pt_device.h kTriTableWords) */
+    bool table_dirty = ctx->tri_table.size() < W * n;
+    if (table_dirty) ctx->tri_table.resize(W * n, 0);
+    uint64_t tris_all = 0, leaves_all = 0;
     for (uint32_t d = 0; d < n; d++) {
         TriRecords& t = ctx->tri[d];
         const uint64_t vb = dc[d].vertexBuffer, ib = dc[d].indexBuffer;
@@ -224,7 +233,8 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         const bool reuse = ctx->tri_cache && t.valid && t.vb == vb && t.ib == ib && t.ntri == ntri && t.gen_vb == gv &&
                            t.gen_ib == gi && gv != kUnknownGeneration && gi != kUnknownGeneration;
         if (!reuse) {
-            const uint64_t bytes = (uint64_t)(ntri ? ntri : 1u) * wcpt::kTriRecordBytes;
+            const uint64_t singles = ((uint64_t)ntri * wcpt::kSingleRecordBytes + 255u) & ~255ull;
+            const uint64_t bytes = singles + ((uint64_t)ntri / 2u + 1u) * wcpt::kPairRecordBytes;
             if (t.cap < bytes) {
                 if (t.mem) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
                 if (t.mem) (void)hipFree(t.mem);
@@ -235,8 +245,10 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
             }
             if (ntri && (vb == 0 || ib == 0))
                 return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "draw command %u: null vertex/index buffer", d);
+            t.pair_offset = singles;
             HIP_TRY(ctx, wcpt::launch_build_tri_records(reinterpret_cast<const uint32_t*>(ib),
-                                                        reinterpret_cast<const float*>(vb), ntri, t.mem, ctx->stream),
+                                                        reinterpret_cast<const float*>(vb), ntri, t.mem,
+                                                        static_cast<char*>(t.mem) + singles, ctx->stream),
                     "build_tri_records");
             t.vb = vb;
             t.ib = ib;
@@ -246,11 +258,16 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
             t.valid = true;
         }
         const uint64_t addr = reinterpret_cast<uint64_t>(t.mem);
-        if (ctx->tri_table[2ull * d] != addr || ctx->tri_table[2ull * d + 1] != ntri) {
-            ctx->tri_table[2ull * d] = addr;
-            ctx->tri_table[2ull * d + 1] = ntri;
-            table_dirty = true;
+        const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, 0};
+        for (uint64_t w = 0; w < W; w++) {
+            if (ctx->tri_table[W * d + w] != entry[w]) {
+                ctx->tri_table[W * d + w] = entry[w];
+                table_dirty = true;
+            }
         }
+        Buffer* bb = buffer_at(ctx, dc[d].bvhBuffer, o);
+        tris_all += ntri;
+        leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
     }
     if (ctx->tri_table_cap < n) {
         if (ctx->d_tri_table) {
@@ -259,16 +276,18 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         }
         ctx->d_tri_table = nullptr;
         ctx->tri_table_cap = 0;
-        HIP_TRY(ctx, hipMalloc(&ctx->d_tri_table, 2ull * n * sizeof(uint64_t)), "hipMalloc(triangle record table)");
+        HIP_TRY(ctx, hipMalloc(&ctx->d_tri_table, W * n * sizeof(uint64_t)), "hipMalloc(triangle record table)");
         ctx->tri_table_cap = n;
         table_dirty = true;
     }
     if (table_dirty) {
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_tri_table, ctx->tri_table.data(), 2ull * n * sizeof(uint64_t),
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_tri_table, ctx->tri_table.data(), W * n * sizeof(uint64_t),
                                     hipMemcpyHostToDevice, ctx->stream), "hipMemcpyAsync(triangle record table)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(triangle record table)");
     }
     a.tri_records = ctx->d_tri_table;
+    a.pair_records = ctx->pair_records == 1 ||
+                     (ctx->pair_records < 0 && leaves_all > 0 && (double)tris_all >= kPairMinTrianglesPerLeaf * leaves_all);
     return WCPT_SUCCESS;
 }
 
@@ -299,6 +318,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.status = ctx->d_status;
     a.counters = ctx->d_counters;
     a.tri_records = nullptr;
+    a.pair_records = false;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ctx->profiling && mode == wcpt::kModeRender) {
         if (ctx->events_used == ctx->events.size()) {
@@ -444,6 +464,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     switch (option) {
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_PAIR_RECORDS:
+        if (value < -1 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pair records %d", value);
+        ctx->pair_records = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_TRIANGLE_CACHE:
         ctx->tri_cache = value ? 1 : 0;

@@ -13,6 +13,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libwcpt.so")
+# Kernel-variant experiments (tools/ab_build.sh) point this at another in-tree build of the same sources.
+LIB_PATH = os.environ.get("WCPT_LIBRARY", LIB_PATH)
 
 WCPT_SUCCESS = 0
 ERRORS = {
@@ -43,6 +45,7 @@ OPTION_DIAGNOSTICS = 2
 OPTION_SORT_RAYS = 3
 OPTION_WF_STACK = 4
 OPTION_TRIANGLE_CACHE = 5
+OPTION_PAIR_RECORDS = 6
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
