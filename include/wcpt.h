@@ -219,6 +219,15 @@ int      wcpt_set_external_image(wcpt_context* ctx, uint64_t device_ptr, uint64_
 int      wcpt_readback(wcpt_context* ctx, float* dst, uint64_t bytes);
 int      wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes); /* seed accumulation */
 
+/* ---- display step after the path (composite.comp:3-54) ------------------------ */
+/* Gamma 1/2.2 + PBR Neutral tonemap of the accumulation image (this context's rows) into caller-owned device
+ * memory at `dst` (e.g. wcpt_buffer_device_address of a buffer of width*rows*16 or *4 bytes). Asynchronous on
+ * the context's stream. RGBA32F is what composite.comp stores; RGBA8 (UNORM, round to nearest) is the display
+ * format (4x fewer bytes for readback or a multi-GPU gather). */
+#define WCPT_COMPOSITE_RGBA32F 0
+#define WCPT_COMPOSITE_RGBA8   1
+int      wcpt_composite(wcpt_context* ctx, uint64_t dst, int format);
+
 /* ---- dispatch ---------------------------------------------------------------------------------------- */
 /* The push block of pathTracer.comp:90-95 minus `sdp`: SceneData travels by value. Asynchronous on the
  * context's stream; the caller owns renderedFramesCount sequencing (PathTracingRenderer.jai:423). */

@@ -51,6 +51,8 @@ def _load():
     lib.oracle_render.restype = C.c_int
     lib.oracle_render.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                   C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(_Counters)]
+    lib.oracle_composite.restype = None
+    lib.oracle_composite.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     lib.oracle_bvh_build.restype = C.c_uint32
     lib.oracle_bvh_build.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
     return lib
@@ -165,3 +167,13 @@ def render_scene(scene, width, height, max_bounce=3, samples=1, frame=0, y0=0, r
     meshes = [(m.positions, m.indices, m.nodes) for m in scene.meshes]
     return render(sd, scene.materials, scene.spheres, meshes, width, height, y0=y0, rows=rows, image=image,
                   threads=threads)
+
+
+def composite(img: np.ndarray):
+    """composite.comp (gamma 1/2.2 + PBR Neutral) of a float4 image: returns (rgba32f, rgba8)."""
+    a = np.ascontiguousarray(img, dtype=np.float32)
+    n = a.size // 4
+    out32 = np.empty(a.shape, dtype=np.float32)
+    out8 = np.empty(a.shape, dtype=np.uint8)
+    lib.oracle_composite(a.ctypes.data, n, out32.ctypes.data, out8.ctypes.data)
+    return out32, out8

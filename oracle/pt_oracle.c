@@ -569,3 +569,65 @@ uint32_t oracle_bvh_build(const float* positions, uint32_t* indices, uint32_t in
     Subdivide(&B, 0, 32);
     return B.overflow ? 0 : B.nodesUsed;
 }
+
+/* ---- composite.comp:3-54 (display step) ------------------------------------------
+ * Restated here independently of the product's wcpt_composite.h; only log/exp are the shared deterministic
+ * definitions (pow(x, y) = exp(y * log(x)); GLSL leaves pow's precision to the driver). */
+static v3 oracle_pbr_neutral(v3 color)                       /* composite.comp:3-23 */
+{
+    const float startCompression = 0.8f - 0.04f;
+    const float desaturation = 0.15f;
+    float x = fminf(color.x, fminf(color.y, color.z));
+    float offset = x < 0.08f ? x - 6.25f * x * x : 0.04f;
+    color.x -= offset;
+    color.y -= offset;
+    color.z -= offset;
+    float peak = fmaxf(color.x, fmaxf(color.y, color.z));
+    if (peak < startCompression) return color;
+    const float d = 1.0f - startCompression;
+    float newPeak = 1.0f - d * d / (peak + d - startCompression);
+    float s = newPeak / peak;
+    color.x *= s;
+    color.y *= s;
+    color.z *= s;
+    float g = 1.0f - 1.0f / (desaturation * (peak - newPeak) + 1.0f);
+    /* GLSL mix(x, y, a) = x * (1 - a) + y * a, y = newPeak * vec3(1) */
+    v3 r;
+    r.x = color.x * (1.0f - g) + newPeak * g;
+    r.y = color.y * (1.0f - g) + newPeak * g;
+    r.z = color.z * (1.0f - g) + newPeak * g;
+    return r;
+}
+
+static float oracle_pow(float x, float y) { return wcpt_expf(y * wcpt_logf(x)); }
+
+/* img: n float4 texels; out32 (n float4) and/or out8 (n RGBA8), either may be NULL */
+void oracle_composite(const float* img, uint64_t n, float* out32, uint8_t* out8)
+{
+    const float gamma = 1.0f / 2.2f;
+    for (uint64_t i = 0; i < n; i++) {
+        v3 c;
+        c.x = oracle_pow(img[4 * i + 0], gamma);               /* composite.comp:47-48 */
+        c.y = oracle_pow(img[4 * i + 1], gamma);
+        c.z = oracle_pow(img[4 * i + 2], gamma);
+        c = oracle_pbr_neutral(c);                             /* :50-51 */
+        if (out32) {
+            out32[4 * i + 0] = c.x;
+            out32[4 * i + 1] = c.y;
+            out32[4 * i + 2] = c.z;
+            out32[4 * i + 3] = 1.0f;                           /* :53 */
+        }
+        if (out8) {
+            const float v[3] = {c.x, c.y, c.z};
+            for (int k = 0; k < 3; k++) {
+                float f = v[k];
+                uint8_t u;
+                if (!(f > 0.0f)) u = 0;
+                else if (f >= 1.0f) u = 255;
+                else u = (uint8_t)(int)(f * 255.0f + 0.5f);
+                out8[4 * i + k] = u;
+            }
+            out8[4 * i + 3] = 255;
+        }
+    }
+}

@@ -355,3 +355,36 @@ def test_record_formats_match_oracle(gpu_ctx, pairs, name, W, H):
     ref, rcnt = oracle.render_scene(s, W, H, max_bounce=3, threads=8)
     assert_close(img, ref)
     assert cnt == rcnt
+
+
+# ---- composite.comp (display step) ---------------------------------------------------
+@pytest.mark.parametrize("rgba8", [False, True])
+def test_composite_matches_oracle(gpu_ctx, rgba8):
+    """Device gamma + PBR Neutral tonemap equals the oracle bit-for-bit, on a rendered frame and on synthetic HDR
+    values covering the tonemap's branches (x < 0.08, peak < 0.76, compression, > 1, 0, NaN, inf, negative)."""
+    rng = np.random.default_rng(11)
+    W, H = 72, 40
+    s = get_scene("cornell")
+    img, _ = gpu_render(gpu_ctx, s, W, H, bounces=3)
+    hdr = np.ones((H, W, 4), np.float32)
+    hdr[..., :3] = (rng.random((H, W, 3)) ** 4 * 16.0).astype(np.float32)
+    hdr[0, :6, :3] = [[0, 0, 0], [1, 1, 1], [np.nan, 0.5, 0.5], [np.inf, 0, 0], [-1, 0.2, 0.2], [0.05, 0.07, 0.9]]
+    nbytes = W * H * (4 if rgba8 else 16)
+    buf = gpu_ctx.buffer_alloc(nbytes)
+    try:
+        gpu_ctx.create_screen(W, H)
+        for src in (img, hdr):
+            gpu_ctx.image_upload(src)
+            gpu_ctx.composite(gpu_ctx.buffer_address(buf), rgba8=rgba8)
+            gpu_ctx.sync()
+            raw = gpu_ctx.buffer_download(buf, nbytes)
+            ref32, ref8 = oracle.composite(src)
+            if rgba8:
+                assert np.array_equal(np.frombuffer(raw, np.uint8).reshape(H, W, 4), ref8)
+            else:
+                got = np.frombuffer(raw, np.float32).reshape(H, W, 4)
+                nan = np.isnan(ref32)
+                assert np.array_equal(np.isnan(got), nan)   # NaN payloads are not compared (x86 vs AMD)
+                assert np.array_equal(got.view(np.uint32)[~nan], ref32.view(np.uint32)[~nan])
+    finally:
+        gpu_ctx.buffer_free(buf)

@@ -146,3 +146,47 @@ def test_row_blocks_compose():
     top, _ = oracle.render_scene(s, 40, 30, max_bounce=3, y0=0, rows=13)
     bot, _ = oracle.render_scene(s, 40, 30, max_bounce=3, y0=13, rows=17)
     assert np.array_equal(np.concatenate([top, bot]), full)
+
+
+# ---- composite.comp (display step) ----------------------------------------------------------------------
+def _composite_f64(img):
+    """float64 restatement of composite.comp:3-54 (gamma 1/2.2 + PBR Neutral) for tolerance checks."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return _composite_f64_body(img)
+
+
+def _composite_f64_body(img):
+    c = np.power(np.maximum(img[..., :3].astype(np.float64), 0.0), 1.0 / 2.2)
+    x = c.min(axis=-1, keepdims=True)
+    off = np.where(x < 0.08, x - 6.25 * x * x, 0.04)
+    c = c - off
+    peak = c.max(axis=-1, keepdims=True)
+    sc = 0.8 - 0.04
+    d = 1.0 - sc
+    new_peak = 1.0 - d * d / (peak + d - sc)
+    g = 1.0 - 1.0 / (0.15 * (peak - new_peak) + 1.0)
+    comp = c * (new_peak / peak)
+    comp = comp * (1.0 - g) + new_peak * g
+    return np.where(peak < sc, c, comp)
+
+
+def test_composite_oracle_vs_float64():
+    rng = np.random.default_rng(3)
+    img = np.ones((64, 48, 4), np.float32)
+    img[..., :3] = (rng.random((64, 48, 3)) ** 3 * 8.0).astype(np.float32)
+    img[0, 0, :3] = [0.0, 0.0, 0.0]
+    img[0, 1, :3] = [1.0, 1.0, 1.0]
+    img[0, 2, :3] = [100.0, 0.5, 0.0]
+    out32, out8 = oracle.composite(img)
+    ref = _composite_f64(img)
+    assert np.all(out32[..., 3] == 1.0) and np.all(out8[..., 3] == 255)
+    np.testing.assert_allclose(out32[..., :3], ref, rtol=2e-6, atol=2e-7)
+    expect8 = np.where(out32[..., :3] > 0, np.floor(np.clip(out32[..., :3], 0, 1) * np.float32(255) + np.float32(0.5)), 0)
+    assert np.array_equal(out8[..., :3], expect8.astype(np.uint8))
+
+
+def test_composite_special_values():
+    img = np.array([[np.nan, 0.5, 0.5, 1], [-1.0, 0.2, 0.2, 1], [np.inf, 0.0, 0.0, 1]], np.float32)
+    out32, out8 = oracle.composite(img)
+    assert out8.dtype == np.uint8 and out8.shape == (3, 4)
+    assert np.all(out8[:, 3] == 255)

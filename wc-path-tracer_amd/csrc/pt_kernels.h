@@ -71,6 +71,8 @@ constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
 constexpr uint32_t kSingleRecordBytes = 48, kPairRecordBytes = 80;
 hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* singles,
                                     void* pairs, hipStream_t stream);
+/* composite.comp (pt_composite.hip): gamma + PBR Neutral over `pixels` float4 texels into rgba32f or RGBA8 */
+hipError_t launch_composite(const float4* img, uint64_t pixels, void* dst, bool rgba8, int cus, hipStream_t stream);
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream);
 /* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
 /* lds_stack: LDS traversal-stack entries per lane of the trace kernel (10, 16 or 24; render mode only). */

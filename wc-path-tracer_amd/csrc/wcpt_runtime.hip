@@ -664,6 +664,29 @@ int wcpt_readback(wcpt_context* ctx, float* dst, uint64_t bytes)
     return read_status(ctx);
 }
 
+int wcpt_composite(wcpt_context* ctx, uint64_t dst, int format)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!ctx->image) return set_error(ctx, WCPT_ERROR_NO_SCREEN, "no output image");
+    if (format != WCPT_COMPOSITE_RGBA32F && format != WCPT_COMPOSITE_RGBA8)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "composite format %d", format);
+    if (!dst) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null composite destination");
+    const uint64_t pixels = (uint64_t)ctx->width * ctx->rows;
+    const uint64_t need = pixels * (format == WCPT_COMPOSITE_RGBA8 ? 4ull : 16ull);
+    uint64_t off = 0;
+    Buffer* b = buffer_at(ctx, dst, off);
+    if (b && off + need > b->bytes)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "composite destination holds %llu bytes, %llu needed",
+                         (unsigned long long)(b->bytes - off), (unsigned long long)need);
+    int dev = 0, cus = 0;
+    HIP_TRY(ctx, hipGetDevice(&dev), "hipGetDevice");
+    HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+    HIP_TRY(ctx, wcpt::launch_composite(ctx->image, pixels, reinterpret_cast<void*>(dst), format == WCPT_COMPOSITE_RGBA8,
+                                        cus, ctx->stream), "composite launch");
+    return WCPT_SUCCESS;
+}
+
 int wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes)
 {
     int rc = bind(ctx);

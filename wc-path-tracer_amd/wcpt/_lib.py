@@ -122,6 +122,7 @@ _PROTOTYPES = {
     "wcpt_set_external_image": (_i, [_p, _u64, _u64]),
     "wcpt_readback": (_i, [_p, _p, _u64]),
     "wcpt_image_upload": (_i, [_p, _p, _u64]),
+    "wcpt_composite": (_i, [_p, _u64, _i]),
     "wcpt_render": (_i, [_p, _p, _u64, _u64, _u64]),
     "wcpt_sync": (_i, [_p]),
     "wcpt_render_counters": (_i, [_p, _p, _u64, _u64, _u64, C.POINTER(Counters)]),

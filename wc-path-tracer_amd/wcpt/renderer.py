@@ -121,6 +121,10 @@ class Context:
         self._chk(lib.wcpt_image_upload(self.h, ptr(a), a.nbytes))
 
     # -- dispatch ---------------------------------------------------------------------------------------
+    def composite(self, dst: int, rgba8: bool = False):
+        """composite.comp into device memory at `dst` (asynchronous)."""
+        self._chk(lib.wcpt_composite(self.h, dst, 1 if rgba8 else 0))
+
     def render(self, sd: np.ndarray, materials: int, spheres: int, draws: int):
         sd = np.ascontiguousarray(sd, dtype=SCENE_DATA_DTYPE)
         self._chk(lib.wcpt_render(self.h, ptr(sd), materials, spheres, draws))
