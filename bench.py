@@ -93,24 +93,38 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 re-renders the timed frame sequence on the full frame and checks the gathered "
+                         "row blocks against it bit-for-bit (adds 'verified' to the JSON line)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the product path) or gloo (host-staged; for rehearsing N>1 "
+                         "ranks on one GPU, where RCCL refuses duplicate devices)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    device = local % max(1, torch.cuda.device_count())  # == local on a node with >= N GPUs
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     name, W, H, spp, bounces, desc = CONFIGS[args.config]
     if args.kernel < 0:
         args.kernel = DEFAULT_KERNEL[args.config]
     scene = wscene.generate(name)
     y0, rows = row_block(H, world, rank)
-    stream = torch.cuda.current_stream()
+    # One explicit stream for everything: the renders (wcpt), the shard copies and the collective. Torch's
+    # default current stream is the legacy null stream (handle 0), which wcpt_set_stream takes as "use the
+    # context's own stream" -- that would leave the gather unordered with the render.
+    stream = torch.cuda.Stream(device=device)
+    torch.cuda.set_stream(stream)
 
-    ctx = wcpt.Context(local)
+    ctx = wcpt.Context(device)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_kernel(args.kernel)
     dev = wcpt.DeviceScene(ctx, scene)
@@ -119,13 +133,15 @@ def main():
     max_rows = -(-H // world)
     shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
     ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
-    gathered = [torch.empty_like(shard) for _ in range(world)] if (world > 1 and rank == 0) else None
+    host_staged = world > 1 and args.dist_backend == "gloo"
+    gather_like = shard.cpu() if host_staged else shard
+    gathered = [torch.empty_like(gather_like) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     def step(frame):
         sd = scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=frame)
         ctx.render(sd, *dev.addresses())
         if world > 1:
-            dist.gather(shard, gathered, dst=0)
+            dist.gather(shard.cpu() if host_staged else shard, gathered, dst=0)
 
     for f in range(args.warmup):
         step(f)
@@ -153,7 +169,7 @@ def main():
         for n in tot:
             tot[n] += c[n]
     t = torch.tensor([elapsed, float(tot["segments"]), float(tot["pixels"] * spp)], dtype=torch.float64,
-                     device="cuda")
+                     device="cpu" if host_staged else "cuda")
     if world > 1:
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -162,6 +178,30 @@ def main():
         elapsed_max, segs_all, prim_all = float(tmax[0]), float(tsum[0]), float(tsum[1])
     else:
         elapsed_max, segs_all, prim_all = elapsed, float(t[1]), float(t[2])
+
+    verified = None
+    if args.verify and rank == 0:
+        if world > 1:
+            frame_img = torch.cat([g[:row_block(H, world, r)[1]].to("cpu") for r, g in enumerate(gathered)], 0)
+        else:
+            frame_img = shard[:H].to("cpu")
+        with wcpt.Context(device) as vctx:
+            vdev = wcpt.DeviceScene(vctx, scene)
+            vctx.set_kernel(args.kernel)
+            vctx.create_screen(W, H)
+            for f in range(args.warmup + args.steps):
+                vctx.render(scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f), *vdev.addresses())
+            ref = vctx.readback()
+            vdev.free()
+        same = frame_img.numpy().view(np.uint32) == ref.view(np.uint32)
+        verified = bool(same.all())
+        if not verified:
+            bad_rows = np.nonzero(~same.all(axis=(1, 2)))[0]
+            print(f"verify: {bad_rows.size} of {H} rows differ (first {bad_rows[:8].tolist()}, "
+                  f"last {bad_rows[-4:].tolist()}); pixel fraction {1.0 - same.all(axis=2).mean():.4f}",
+                  file=sys.stderr, flush=True)
+            if os.environ.get("WCPT_VERIFY_DUMP"):
+                np.savez(os.environ["WCPT_VERIFY_DUMP"], got=frame_img.numpy(), ref=ref)
 
     if rank == 0:
         ms_per_step = elapsed_max / args.steps * 1e3
@@ -193,7 +233,8 @@ def main():
             "config": {"workload": desc, "config": args.config, "scene": name, "width": W, "height": H,
                        "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel],
-                       "parallelism": f"row-block x{world}" + (" + RCCL gather" if world > 1 else "")},
+                       "parallelism": f"row-block x{world}" + ((" + RCCL gather" if args.dist_backend == "nccl"
+                                                               else " + gloo gather (rehearsal)") if world > 1 else "")},
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
             "segments_per_frame": int(segs_all / args.steps),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
@@ -201,6 +242,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(bytes_per_launch)},
         }
+        if verified is not None:
+            out["verified"] = verified
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, W, H, spp, bounces, budget_s=args.cpu_seconds)
             out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)

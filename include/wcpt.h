@@ -206,6 +206,7 @@ uint64_t wcpt_buffer_device_address(wcpt_context* ctx, wcpt_buffer buf); /* 0 on
 int      wcpt_buffer_free(wcpt_context* ctx, wcpt_buffer buf);
 
 /* ---- output image (CreateScreen / Resize) --------------------------------------------------------- */
+/* The context-owned image starts as zeros (the reference's is undefined; its editor blends frame 1 with it). */
 int      wcpt_create_screen(wcpt_context* ctx, uint32_t width, uint32_t height);
 int      wcpt_resize(wcpt_context* ctx, uint32_t width, uint32_t height);
 /* Row-block shard: this context renders and stores only rows [y0, y0+rows) of the width x height

@@ -602,7 +602,15 @@ int wcpt_create_screen(wcpt_context* ctx, uint32_t width, uint32_t height)
     } else {
         ctx->sharded = false;
     }
-    return alloc_image(ctx, width, height, y0, rows);
+    rc = alloc_image(ctx, width, height, y0, rows);
+    if (rc) return rc;
+    /* The reference's storage image starts undefined (PathTracingRenderer.jai:345-385) and its editor's first
+     * frame already blends with it (renderedFramesCount 1, editor.jai:149-152): define it as zero. */
+    if (!ctx->external_bytes) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->image, 0, (uint64_t)width * rows * 16ull, ctx->stream), "hipMemsetAsync(image)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    }
+    return WCPT_SUCCESS;
 }
 
 int wcpt_resize(wcpt_context* ctx, uint32_t width, uint32_t height)

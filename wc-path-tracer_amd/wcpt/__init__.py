@@ -6,14 +6,14 @@ package is the Python host mirror used by tests and the benchmark.
 from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL,
                    KERNEL_WAVEFRONT, LIB_PATH, MATERIAL_DIELECTRIC, MATERIAL_DTYPE, MATERIAL_METAL, NODE_DTYPE,
                    SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, WcptError, lib)
-from .renderer import Context, DeviceScene, PathTracingRenderer
+from .renderer import Context, DeviceScene, Editor, PathTracingRenderer
 from . import scene
 
 __all__ = [
     "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
-    "PathTracingRenderer", "scene", "device_count",
+    "PathTracingRenderer", "Editor", "scene", "device_count",
 ]
 
 

@@ -302,4 +302,34 @@ class PathTracingRenderer:
         self.ctx.close()
 
 
-__all__ = ["Context", "DeviceScene", "PathTracingRenderer", "COUNTER_FIELDS"]
+class Editor:
+    """The editor's per-frame protocol around the renderer (src/editor.jai:118-158), for frame sequencing:
+
+    - camera input: ``moved`` resets ``renderedFramesCount`` to 0, otherwise the editor adds 1 (:149-152);
+    - UpdateEditor (:154-158): camera Update (aspect of the viewport), UpdateMaterials, Render, which uploads
+      SceneData with the current count and adds its own 1 (PathTracingRenderer.jai:423).
+
+    So while the camera is still the shader sees every second frame number (1, 3, 5, ... from start-up; 0, 2,
+    4, ... after a move), and the progressive ``mix`` weights follow that sequence. ``frame`` returns the
+    count the dispatch used.
+    """
+
+    def __init__(self, renderer: PathTracingRenderer, camera: Camera):
+        self.renderer = renderer
+        self.camera = camera
+
+    def frame(self, moved: bool = False) -> int:
+        r = self.renderer
+        if moved:
+            r.renderedFramesCount = 0
+        else:
+            r.renderedFramesCount += 1
+        w, h = r.renderSize
+        cam = _scene.update_camera(self.camera, w / h)
+        r.UpdateMaterials()
+        used = r.renderedFramesCount
+        r.Render(cam)
+        return used
+
+
+__all__ = ["Context", "DeviceScene", "PathTracingRenderer", "Editor", "COUNTER_FIELDS"]
