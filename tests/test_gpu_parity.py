@@ -447,3 +447,46 @@ def test_c_host_editor_loop(gpu_ctx, tmp_path):
         acc, _ = oracle.render_scene(s, W, H, sd=sd, image=acc)
     _, ref8 = oracle.composite(acc)
     assert np.array_equal(rgb, ref8[..., :3])
+
+
+# ---- edge cases of the inputs -------------------------------------------------------------------------------
+def _variant(name, kind):
+    import copy
+    s = copy.copy(get_scene(name))
+    if kind == "no_spheres":
+        s.spheres = s.spheres[:0]
+    elif kind == "no_meshes":
+        s.meshes = []
+    elif kind == "empty":
+        s.spheres = s.spheres[:0]
+        s.meshes = []
+    elif kind == "two_draws":          # the same mesh drawn twice: exercises the per-draw loop (:152-201)
+        s.meshes = [s.meshes[0], s.meshes[0]]
+    elif kind == "all_dielectric":     # type 1 everywhere, with absorption (:263-280)
+        m = s.materials.copy()
+        m["type"] = 1
+        m["ior"] = 1.5
+        m["absorptionStrength"] = 0.7
+        m["absorption"] = [0.2, 0.5, 0.9]
+        s.materials = m
+    return s
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kind,bounces,spp", [
+    ("no_spheres", 3, 1), ("no_meshes", 3, 1), ("empty", 3, 1), ("two_draws", 3, 1),
+    ("all_dielectric", 6, 2), ("base", 0, 1), ("base", 12, 1), ("base", 3, 0),
+])
+def test_edge_inputs_match_oracle(gpu_ctx, kernel, kind, bounces, spp):
+    """Empty sphere / draw lists, an empty scene (sky only), two draw commands, dielectric everywhere,
+    maxBounceCount 0 and 12, and samples = 0 (the reference divides by zero: NaN pixels, :312)."""
+    s = get_scene("cornell") if kind == "base" else _variant("cornell", kind)
+    W, H = 40, 24
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, kernel=kernel)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, threads=8)
+    if spp == 0:
+        assert np.isnan(ref[..., :3]).all() and np.isnan(img[..., :3]).all()
+        assert np.array_equal(img[..., 3], ref[..., 3])
+    else:
+        assert_close(img, ref)
+    assert cnt == rcnt
