@@ -72,6 +72,9 @@ extern "C" {
 /* Megakernel leaf tests: -1 (default) choose by mean triangles per leaf; 0 single records; 1 pair records
  * (two triangles per lane with packed-FP32 arithmetic). Results are identical either way. */
 #define WCPT_OPTION_PAIR_RECORDS 6
+/* Traversal stack entries carry the deferred child's (left, count) (1, default, when the draw's BVH buffer is a
+ * context buffer of < 2^24 nodes) so a pop needs no node fetch; 0: entries hold node indices. Same results. */
+#define WCPT_OPTION_PACKED_REFS 7
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

@@ -490,3 +490,31 @@ def test_edge_inputs_match_oracle(gpu_ctx, kernel, kind, bounces, spp):
     else:
         assert_close(img, ref)
     assert cnt == rcnt
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("refs", [1, 0])
+def test_stack_refs_match_oracle(gpu_ctx, kernel, refs):
+    """Stack entries carrying (left, count) (default) or node indices: same frame, same counters. The hand-made
+    BVH below has fat leaves (count 300 >= 255 index units) as deferred children: the packed form's fetch escape."""
+    rng = np.random.default_rng(5)
+    ntri = 200
+    pos = (rng.random((ntri * 3, 3), dtype=np.float32) * 2.0 - 1.0).astype(np.float32)
+    pos[:, 2] -= 3.0
+    idx = np.arange(ntri * 3, dtype=np.uint32)
+    lo0, hi0 = pos[:300].min(axis=0), pos[:300].max(axis=0)
+    lo1, hi1 = pos[300:].min(axis=0), pos[300:].max(axis=0)
+    nodes = np.zeros(3, dtype=wcpt._lib.NODE_DTYPE)
+    nodes[0] = (np.minimum(lo0, lo1), np.maximum(hi0, hi1), 1, 0)
+    nodes[1] = (lo0, hi0, 0, 300)
+    nodes[2] = (lo1, hi1, 300, 300)
+    fat = _with_mesh(get_scene("default"), wscene.HostBVH(pos, idx, nodes))
+    gpu_ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, refs)
+    try:
+        for s, (W, H) in ((get_scene("atrium"), (64, 40)), (get_scene("cornell"), (48, 32)), (fat, (48, 40))):
+            img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=3, kernel=kernel)
+            ref, rcnt = oracle.render_scene(s, W, H, max_bounce=3, threads=8)
+            assert_close(img, ref)
+            assert cnt == rcnt
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, 1)

@@ -146,6 +146,22 @@ __device__ __forceinline__ uint2 load_node_lc(gnode_ptr bvh, uint32_t i)
     const v2u v = reinterpret_cast<const WCPT_GLOBAL v2u*>(bvh + i)[3];
     return make_uint2(v.x, v.y);
 }
+/* Stack entry node references. Packed form (draws whose BVH has < 2^24 nodes and whose index count is < 2^24,
+ * table flag kTriFlagPackedRefs): the deferred child's own (left, count) as (left << 8) | count when count < 255,
+ * so that popping it needs no node fetch -- the pop path then has no dependent memory round trip; otherwise
+ * (node index << 8) | 255 and the node's (left, count) is fetched at pop. Unpacked form: the node index. */
+constexpr uint32_t kRefFetch = 255u;
+__device__ __forceinline__ uint32_t node_ref(bool packed, uint32_t node_index, uint32_t left, uint32_t count)
+{
+    if (!packed) return node_index;
+    return (count < kRefFetch && left < (1u << 24)) ? (left << 8) | count : (node_index << 8) | kRefFetch;
+}
+__device__ __forceinline__ uint2 node_ref_lc(bool packed, gnode_ptr bvh, uint32_t ref)
+{
+    if (!packed) return load_node_lc(bvh, ref);
+    if ((ref & 255u) != kRefFetch) return make_uint2(ref >> 8, ref & 255u);
+    return load_node_lc(bvh, ref >> 8);
+}
 __device__ __forceinline__ void node_box(const Ray& r, const NodeV& n, float& t0, float& t1)
 {
     /* node = {min.xyz, max.x | max.yz, left, count} */
@@ -193,8 +209,9 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { r
  * The reference's BVH keeps each leaf's index triples contiguous (PathTracingRenderer.jai:233), so a leaf's
  * records are contiguous. A leaf whose first index position is not a multiple of 3 (never produced by the
  * reference's builder) or that reaches past the draw's indexCount uses the index path.
- * Per-draw table entry: {single record address, pair record address, triangle count, -} (4 x u64). */
+ * Per-draw table entry: {single record address, pair record address, triangle count, flags} (4 x u64). */
 constexpr uint32_t kTriTableWords = 4;
+constexpr uint64_t kTriFlagPackedRefs = 1u; /* table word 3: stack entries may carry (left, count) */
 typedef const WCPT_GLOBAL v4f* gtri_ptr;
 struct TriE { f3 a, e1, e2; };
 __device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
@@ -427,6 +444,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         const gf32_ptr vertices = as_f32(draws[i].vertexBuffer);
         const gtri_ptr tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + (PAIRS ? 1u : 0u)];
         const uint32_t ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
+        const bool packed = (tri_records[kTriTableWords * i + 3u] & kTriFlagPackedRefs) != 0u;
         if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
 
         /* root: pushed untested, popped and tested (:155-162) */
@@ -507,7 +525,8 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 const bool passFar = leftFirst ? passR : passL;
                 const float nearT0 = leftFirst ? l0 : r0;
                 const float farT0 = leftFirst ? r0 : l0;
-                if (passFar && !stk.push(farIdx, farT0)) overflow = true;
+                const NodeV& F = leftFirst ? R : L;
+                if (passFar && !stk.push(node_ref(packed, farIdx, F.b.z, F.b.w), farT0)) overflow = true;
                 if (passNear && !(nearT0 > rt)) {
                     const NodeV& N = leftFirst ? L : R;
                     curLeft = N.b.z;
@@ -522,7 +541,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 float t0;
                 stk.pop(ni, t0);
                 if (t0 > rt) continue;
-                const uint2 lc = load_node_lc(bvh, ni);
+                const uint2 lc = node_ref_lc(packed, bvh, ni);
                 curLeft = lc.x;
                 curCount = lc.y;
                 found = true;

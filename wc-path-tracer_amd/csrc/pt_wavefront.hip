@@ -151,6 +151,7 @@ enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 
 struct Geom {
     gtri_ptr tris;
     uint32_t ntri;
+    bool packed; /* stack entries carry (left, count): kTriFlagPackedRefs */
     gnode_ptr bvh;
     gu32_ptr indices;
     gf32_ptr vertices;
@@ -162,6 +163,7 @@ __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ 
     Geom g;
     g.tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * d];      /* single records */
     g.ntri = (uint32_t)tri_records[kTriTableWords * d + 2u];
+    g.packed = (tri_records[kTriTableWords * d + 3u] & kTriFlagPackedRefs) != 0u;
     g.bvh = as_nodes(draws[d].bvhBuffer);
     g.indices = as_u32(draws[d].indexBuffer);
     g.vertices = as_f32(draws[d].vertexBuffer);
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     stk.sp = 0;
     Counters cnt = {};
     bool overflow = false;
-    Geom g0 = {nullptr, 0u, nullptr, nullptr, nullptr}, gl = {nullptr, 0u, nullptr, nullptr, nullptr};
+    Geom g0 = {nullptr, 0u, false, nullptr, nullptr, nullptr}, gl = {nullptr, 0u, false, nullptr, nullptr, nullptr};
     if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
 
     bool has = false, drained = false;
@@ -319,7 +321,11 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 const bool leftFirst = leftDist < rightDist;
                 const bool passNear = leftFirst ? passL : passR;
                 const bool passFar = leftFirst ? passR : passL;
-                if (passFar && !stk.push(leftFirst ? ca + 1 : ca, leftFirst ? r0 : l0)) overflow = true;
+                if (passFar) {
+                    const NodeV& F = leftFirst ? R : L;
+                    if (!stk.push(node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w), leftFirst ? r0 : l0))
+                        overflow = true;
+                }
                 if (passNear && !((leftFirst ? l0 : r0) > rt)) {
                     const uint32_t nl = leftFirst ? L.b.z : R.b.z, nc = leftFirst ? L.b.w : R.b.w;
                     cursor_from(nl, nc, g.ntri, ca, cb, cr, mode);
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     float t0;
                     stk.pop(ni, t0);
                     if (t0 > rt) continue;
-                    const uint2 lc = load_node_lc(g.bvh, ni);
+                    const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
                     cursor_from(lc.x, lc.y, g.ntri, ca, cb, cr, mode);
                     found = true;
                     break;

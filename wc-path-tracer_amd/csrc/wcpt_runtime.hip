@@ -99,6 +99,7 @@ struct wcpt_context {
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
+    int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
     std::vector<TriRecords> tri;       /* per draw command index */
@@ -258,14 +259,18 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
             t.valid = true;
         }
         const uint64_t addr = reinterpret_cast<uint64_t>(t.mem);
-        const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, 0};
+        /* stack entries may carry the child's (left, count) when every node index and index position fits in 24
+         * bits (pt_device.h node_ref); unknown BVH size -> node-index entries */
+        Buffer* bb = buffer_at(ctx, dc[d].bvhBuffer, o);
+        const uint64_t nodes = bb ? (bb->bytes - o) / sizeof(wcpt_node) : ~0ull;
+        const uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
+        const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, flags};
         for (uint64_t w = 0; w < W; w++) {
             if (ctx->tri_table[W * d + w] != entry[w]) {
                 ctx->tri_table[W * d + w] = entry[w];
                 table_dirty = true;
             }
         }
-        Buffer* bb = buffer_at(ctx, dc[d].bvhBuffer, o);
         tris_all += ntri;
         leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
     }
@@ -464,6 +469,9 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     switch (option) {
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_PACKED_REFS:
+        ctx->packed_refs = value ? 1 : 0;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PAIR_RECORDS:
         if (value < -1 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pair records %d", value);

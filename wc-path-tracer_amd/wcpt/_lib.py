@@ -46,6 +46,7 @@ OPTION_SORT_RAYS = 3
 OPTION_WF_STACK = 4
 OPTION_TRIANGLE_CACHE = 5
 OPTION_PAIR_RECORDS = 6
+OPTION_PACKED_REFS = 7
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
