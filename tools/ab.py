@@ -60,6 +60,7 @@ def main():
             ctx.set_option(wcpt._lib.OPTION_WF_STACK, int(o.get("lds", 10)))
             ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, int(o.get("pairs", -1)))
             ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, int(o.get("refs", 1)))
+            ctx.set_option(wcpt._lib.OPTION_WF_REFILL, int(o.get("refill", 12)))
             dev = scenes[o.get("deindex", "0")]
             ctx.profile_begin()
             for sd in sds:

@@ -24,6 +24,7 @@ struct LaunchArgs {
     const wcpt_draw_command* draws;
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
+    uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
     float4* image;
     uint32_t W, H, y0, rows;
     uint32_t* status;

@@ -199,7 +199,8 @@ template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
 __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
                                                   const wcpt_draw_command* __restrict__ draws,
                                                   const uint64_t* __restrict__ tri_records, WfBuffers b,
-                                                  uint32_t* __restrict__ status, unsigned long long* __restrict__ counters)
+                                                  uint32_t* __restrict__ status, unsigned long long* __restrict__ counters,
+                                                  uint32_t refill)
 {
     __shared__ uint64_t s_stack[LDSN * 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.count_out = 0; /* shade appends to it after this kernel */
@@ -242,9 +243,10 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     };
 
     for (;;) {
-        /* dynamic fetch: idle lanes take the next queued rays */
-        if (!drained) {
-            unsigned long long need = __ballot(!has);
+        /* dynamic fetch: idle lanes take the next queued rays, once at least `refill` lanes are idle (or none
+         * has work left) */
+        unsigned long long need = __ballot(!has);
+        if (!drained && ((uint32_t)__popcll(need) >= refill || need == ~0ull)) {
             while (need) {
                 if (lo == hi) {
                     uint32_t base = 0;
@@ -553,7 +555,7 @@ static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace
                          hipStream_t stream)
 {
     hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
-                       a.tri_records, b, a.status, a.counters);
+                       a.tri_records, b, a.status, a.counters, a.wf_refill);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
                        a.spheres, a.draws, b, a.image, a.W, a.H, a.y0, a.counters);
 }

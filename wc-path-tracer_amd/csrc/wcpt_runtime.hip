@@ -100,6 +100,7 @@ struct wcpt_context {
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
+    int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (measured optimum 8..16 on c3) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
     std::vector<TriRecords> tri;       /* per draw command index */
@@ -324,6 +325,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.counters = ctx->d_counters;
     a.tri_records = nullptr;
     a.pair_records = false;
+    a.wf_refill = (uint32_t)ctx->wf_refill;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ctx->profiling && mode == wcpt::kModeRender) {
         if (ctx->events_used == ctx->events.size()) {
@@ -469,6 +471,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     switch (option) {
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_WF_REFILL:
+        if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
+        ctx->wf_refill = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PACKED_REFS:
         ctx->packed_refs = value ? 1 : 0;

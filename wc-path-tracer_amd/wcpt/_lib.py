@@ -47,6 +47,7 @@ OPTION_WF_STACK = 4
 OPTION_TRIANGLE_CACHE = 5
 OPTION_PAIR_RECORDS = 6
 OPTION_PACKED_REFS = 7
+OPTION_WF_REFILL = 8
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
