@@ -1,0 +1,45 @@
+// Exhaustive check: is (v_rcp_f32 + one FMA Newton step) the correctly rounded reciprocal for every binary32 x
+// in a given range? Compares against 1.0f / x (hipcc's IEEE division) over all 2^32 bit patterns.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+__global__ void check(unsigned long long* mism, unsigned long long* first, uint32_t hi_bits)
+{
+    const uint64_t base = ((uint64_t)hi_bits << 24);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < (1u << 24); k += gridDim.x * blockDim.x) {
+        const uint32_t bits = (uint32_t)(base + k);
+        const float x = __uint_as_float(bits);
+        const float a = fabsf(x);
+        if (!(a >= 0x1p-126f && a < 0x1p126f)) continue; /* the fast path's guarded range */
+        const float ref = 1.0f / x;
+        const float y = __builtin_amdgcn_rcpf(x);
+        const float e = __builtin_fmaf(-x, y, 1.0f);
+        const float r = __builtin_fmaf(e, y, y);
+        if (__float_as_uint(r) != __float_as_uint(ref)) {
+            atomicAdd(mism, 1ull);
+            atomicMin(first, (unsigned long long)bits);
+        }
+    }
+}
+
+int main()
+{
+    unsigned long long *m, *f;
+    hipMalloc(&m, 8);
+    hipMalloc(&f, 8);
+    unsigned long long total = 0, firstbad = ~0ull;
+    for (uint32_t hb = 0; hb < 256; hb++) {
+        unsigned long long z = 0, ff = ~0ull;
+        hipMemcpy(m, &z, 8, hipMemcpyHostToDevice);
+        hipMemcpy(f, &ff, 8, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(check, dim3(4096), dim3(256), 0, 0, m, f, hb);
+        unsigned long long c = 0, fb = 0;
+        hipMemcpy(&c, m, 8, hipMemcpyDeviceToHost);
+        hipMemcpy(&fb, f, 8, hipMemcpyDeviceToHost);
+        total += c;
+        if (c && fb < firstbad) firstbad = fb;
+    }
+    printf("mismatches %llu first 0x%08llx\n", total, firstbad == ~0ull ? 0ull : firstbad);
+    return total ? 1 : 0;
+}

@@ -161,6 +161,22 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
     case 4: out[i] = __float_as_uint(wcpt_expf(__uint_as_float(a))); break;
     case 5: out[i] = __float_as_uint(sqrtf(__uint_as_float(a))); break;
     case 6: out[i] = __float_as_uint(__uint_as_float(a) / __uint_as_float(in2[i])); break;
+    case 8: { /* exhaustive fast-reciprocal check: mismatches of rcp_exact's fast path vs IEEE 1/x over the 2^16
+                 inputs (a << 16) | k inside the fast path's range */
+        uint32_t bad = 0;
+        for (uint32_t k = 0; k < 65536u; k++) {
+            const float x = __uint_as_float((a << 16) | k);
+            const float ax = fabsf(x);
+            if (!(ax >= 0x1p-126f && ax < 0x1p126f)) continue;
+            const float y = __builtin_amdgcn_rcpf(x);
+            const float e = __builtin_fmaf(-x, y, 1.0f);
+            const float r = __builtin_fmaf(e, y, y);
+            bad += (__float_as_uint(r) != __float_as_uint(1.0f / x)) ? 1u : 0u;
+        }
+        out[i] = bad;
+        break;
+    }
+    case 9: out[i] = __float_as_uint(rcp_exact(__uint_as_float(a))); break;
     case 7: { /* RandomDirection: 3 words per input */
         uint32_t s = a;
         const f3 d = RandomDirection(s);
