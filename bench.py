@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: gather each frame on the render stream instead of overlapping it with the next render")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 re-renders the timed frame sequence on the full frame and checks the gathered "
                          "row blocks against it bit-for-bit (adds 'verified' to the JSON line)")
@@ -135,13 +137,40 @@ def main():
     ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
     host_staged = world > 1 and args.dist_backend == "gloo"
     gather_like = shard.cpu() if host_staged else shard
-    gathered = [torch.empty_like(gather_like) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # Overlap: frame k's row block is copied (on the render stream, 16 B/px, ~2 us) into one of two staging
+    # buffers and gathered on a separate communication stream while frame k+1 renders. Every frame is still
+    # rendered and gathered; the timed region ends with a device-wide synchronize that includes the last gather.
+    overlap = world > 1 and not args.no_overlap
+    comm = torch.cuda.Stream(device=device) if overlap else None
+    staging = [torch.empty_like(shard) for _ in range(2)] if overlap else None
+    gathers_done = [None, None]            # event: the gather that last read staging[i] has finished
+    nbuf = 2 if overlap else 1
+    gathered = [[torch.empty_like(gather_like) for _ in range(world)] for _ in range(nbuf)] \
+        if (world > 1 and rank == 0) else None
+    last = {"buf": 0}
 
     def step(frame):
         sd = scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=frame)
         ctx.render(sd, *dev.addresses())
-        if world > 1:
-            dist.gather(shard.cpu() if host_staged else shard, gathered, dst=0)
+        if world == 1:
+            return
+        i = frame % nbuf
+        last["buf"] = i
+        out = gathered[i] if rank == 0 else None
+        if not overlap:
+            dist.gather(shard.cpu() if host_staged else shard, out, dst=0)
+            return
+        if gathers_done[i] is not None:
+            stream.wait_event(gathers_done[i])          # staging[i] is free again
+        staging[i].copy_(shard, non_blocking=True)       # on the render stream, after this frame's render
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        with torch.cuda.stream(comm):
+            comm.wait_event(ready)
+            dist.gather(staging[i].cpu() if host_staged else staging[i], out, dst=0)
+            done = torch.cuda.Event()
+            done.record(comm)
+        gathers_done[i] = done
 
     for f in range(args.warmup):
         step(f)
@@ -182,7 +211,8 @@ def main():
     verified = None
     if args.verify and rank == 0:
         if world > 1:
-            frame_img = torch.cat([g[:row_block(H, world, r)[1]].to("cpu") for r, g in enumerate(gathered)], 0)
+            frame_img = torch.cat([g[:row_block(H, world, r)[1]].to("cpu")
+                                   for r, g in enumerate(gathered[last["buf"]])], 0)
         else:
             frame_img = shard[:H].to("cpu")
         with wcpt.Context(device) as vctx:
@@ -234,7 +264,9 @@ def main():
                        "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel],
                        "parallelism": f"row-block x{world}" + ((" + RCCL gather" if args.dist_backend == "nccl"
-                                                               else " + gloo gather (rehearsal)") if world > 1 else "")},
+                                                               else " + gloo gather (rehearsal)")
+                                                              + (" overlapped with the next frame" if overlap else "")
+                                                              if world > 1 else "")},
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
             "segments_per_frame": int(segs_all / args.steps),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),

@@ -254,8 +254,11 @@ __device__ __forceinline__ TriPair load_pair(gtri_ptr t, uint32_t j)
     return p;
 }
 __device__ __forceinline__ v2f bc2(float s) { v2f r = {s, s}; return r; }
-/* rayTriangleE for the two triangles of a pair; t.x for triangle 2j, t.y for 2j+1 (-1 = miss). */
-__device__ __forceinline__ v2f rayTrianglePair(const Ray& r, const TriPair& p)
+/* rayTriangleE for the two triangles of a pair: t for triangle 2j (.x) and 2j+1 (.y), and whether each passed
+ * the reference's acceptance test (t > 0, u, v, u + v in range). A triangle is taken iff it passed and t < rec.t;
+ * that equals the reference's `t != -1 && t < rec.t` on its -1-for-miss result (a pass implies t > 0). */
+struct PairHit { v2f t; bool hit0, hit1; };
+__device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& p)
 {
     const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
     const v2f oax = bc2(r.origin.x) - p.ax, oay = bc2(r.origin.y) - p.ay, oaz = bc2(r.origin.z) - p.az;
@@ -275,10 +278,11 @@ __device__ __forceinline__ v2f rayTrianglePair(const Ray& r, const TriPair& p)
     const v2f v = (dx * (qx * inv) + dy * (qy * inv)) + dz * (qz * inv);
     const v2f t = ((p.e2x * qx + p.e2y * qy) + p.e2z * qz) * inv;
     const v2f uv = u + v;
-    v2f res;
-    res.x = (t.x > 0.0f && u.x >= 0.0f && u.x <= 1.0f && v.x >= 0.0f && uv.x <= 1.0f) ? t.x : -1.0f;
-    res.y = (t.y > 0.0f && u.y >= 0.0f && u.y <= 1.0f && v.y >= 0.0f && uv.y <= 1.0f) ? t.y : -1.0f;
-    return res;
+    PairHit h;
+    h.t = t;
+    h.hit0 = t.x > 0.0f && u.x >= 0.0f && u.x <= 1.0f && v.x >= 0.0f && uv.x <= 1.0f;
+    h.hit1 = t.y > 0.0f && u.y >= 0.0f && u.y <= 1.0f && v.y >= 0.0f && uv.y <= 1.0f;
+    return h;
 }
 __device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
 {
@@ -475,14 +479,14 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 if (PAIRS && k0 != kNoRecord) {
                     const uint32_t kend = k0 + (curCount + 2u) / 3u;
                     for (uint32_t k = k0 & ~1u; k < kend; k += 2) {
-                        const v2f tt = rayTrianglePair(ray, load_pair(tris, k >> 1));
+                        const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
                         if (k >= k0) {
                             if (COUNT) {
                                 cnt.triangle_tests++;
                                 simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
                             }
-                            if (tt.x != -1.0f && tt.x < rt) {
-                                rt = tt.x;
+                            if (ph.hit0 && ph.t.x < rt) {
+                                rt = ph.t.x;
                                 prim = 3u * k;
                                 primDraw = i;
                             }
@@ -492,8 +496,8 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                                 cnt.triangle_tests++;
                                 simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
                             }
-                            if (tt.y != -1.0f && tt.y < rt) {
-                                rt = tt.y;
+                            if (ph.hit1 && ph.t.y < rt) {
+                                rt = ph.t.y;
                                 prim = 3u * (k + 1u);
                                 primDraw = i;
                             }
