@@ -98,9 +98,9 @@ def main():
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 re-renders the timed frame sequence on the full frame and checks the gathered "
                          "row blocks against it bit-for-bit (adds 'verified' to the JSON line)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl (= RCCL over xGMI, the product path) or gloo (host-staged; for rehearsing N>1 "
-                         "ranks on one GPU, where RCCL refuses duplicate devices)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo", "gloo-host"],
+                    help="nccl (= RCCL over xGMI, the product path); gloo (device tensors) or gloo-host (host-staged) "
+                         "rehearse N>1 ranks on one GPU, where RCCL refuses duplicate devices")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,7 +135,7 @@ def main():
     max_rows = -(-H // world)
     shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
     ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
-    host_staged = world > 1 and args.dist_backend == "gloo"
+    host_staged = world > 1 and args.dist_backend == "gloo-host"
     gather_like = shard.cpu() if host_staged else shard
     # Overlap: frame k's row block is copied (on the render stream, 16 B/px, ~2 us) into one of two staging
     # buffers and gathered on a separate communication stream while frame k+1 renders. Every frame is still
@@ -264,7 +264,7 @@ def main():
                        "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel],
                        "parallelism": f"row-block x{world}" + ((" + RCCL gather" if args.dist_backend == "nccl"
-                                                               else " + gloo gather (rehearsal)")
+                                                               else f" + {args.dist_backend} gather (rehearsal)")
                                                               + (" overlapped with the next frame" if overlap else "")
                                                               if world > 1 else "")},
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
