@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--bvh", default="midpoint", choices=["midpoint", "sah"],
+                    help="BVH builder: the reference's midpoint split (default: the benchmarked workload) or the "
+                         "optional binned SAH (a different tree, reported as a separate workload)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: gather each frame on the render stream instead of overlapping it with the next render")
     ap.add_argument("--verify", action="store_true",
@@ -118,7 +121,7 @@ def main():
     name, W, H, spp, bounces, desc = CONFIGS[args.config]
     if args.kernel < 0:
         args.kernel = DEFAULT_KERNEL[args.config]
-    scene = wscene.generate(name)
+    scene = wscene.generate(name, bvh=args.bvh)
     y0, rows = row_block(H, world, rank)
     # One explicit stream for everything: the renders (wcpt), the shard copies and the collective. Torch's
     # default current stream is the legacy null stream (handle 0), which wcpt_set_stream takes as "use the
@@ -262,7 +265,7 @@ def main():
             "data": "synthetic (procedural scene generated in-process, no dataset)",
             "config": {"workload": desc, "config": args.config, "scene": name, "width": W, "height": H,
                        "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
-                       "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel],
+                       "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel], "bvh": args.bvh,
                        "parallelism": f"row-block x{world}" + ((" + RCCL gather" if args.dist_backend == "nccl"
                                                                else f" + {args.dist_backend} gather (rehearsal)")
                                                               + (" overlapped with the next frame" if overlap else "")

@@ -263,6 +263,11 @@ void     wcpt_mesh_free(wcpt_mesh* mesh);
  * max_nodes entries; 2*index_count/3 is always enough. */
 int      wcpt_bvh_build(const float* positions, uint32_t vertex_count, uint32_t* indices,
                         uint32_t index_count, wcpt_node* nodes, uint32_t max_nodes, uint32_t* nodes_used);
+/* Optional binned-SAH builder: same node format and conventions, a different tree (far
+ * fewer nodes visited on large meshes). Images equal the midpoint tree's except where two triangles hit at exactly
+ * the same t. Permutes `indices` into leaf order; 2*index_count/3 nodes always suffice. */
+int      wcpt_bvh_build_sah(const float* positions, uint32_t vertex_count, uint32_t* indices,
+                            uint32_t index_count, wcpt_node* nodes, uint32_t max_nodes, uint32_t* nodes_used);
 /* Camera Update (PathTracingRenderer.jai:22-36): yaw/pitch/fov/position -> matrices. */
 int      wcpt_camera_update(wcpt_camera* cam, float aspect_ratio);
 /* Scene generators: "default" (reference Init scene, PathTracingRenderer.jai:322-339, without a mesh),

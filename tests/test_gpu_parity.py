@@ -553,3 +553,23 @@ def test_wavefront_refill_thresholds(gpu_ctx, refill):
     ref, rcnt = oracle.render_scene(s, 80, 48, max_bounce=4, threads=8)
     assert_close(img, ref)
     assert cnt == rcnt
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sah_bvh_frames(gpu_ctx, kernel):
+    """The optional SAH tree through the same kernels: bit-exact against the oracle on the same tree, and equal to
+    the midpoint tree's image except where triangles tie in t (a few pixels at most), with far fewer node visits."""
+    mid = get_scene("atrium")
+    if "atrium_sah" not in _scenes:
+        _scenes["atrium_sah"] = wscene.generate("atrium", bvh="sah")
+    sah = _scenes["atrium_sah"]
+    W, H = 96, 54
+    img, cnt = gpu_render(gpu_ctx, sah, W, H, bounces=4, kernel=kernel)
+    ref, rcnt = oracle.render_scene(sah, W, H, max_bounce=4, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+    img_mid, cnt_mid = gpu_render(gpu_ctx, mid, W, H, bounces=4, kernel=kernel)
+    differ = (img.view(np.uint32) != img_mid.view(np.uint32)).any(axis=2).mean()
+    assert differ <= 0.01, f"{differ:.4f} of pixels differ between SAH and midpoint trees"
+    assert cnt["segments"] == cnt_mid["segments"] or differ > 0
+    assert cnt["interior_visits"] < cnt_mid["interior_visits"]

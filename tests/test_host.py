@@ -177,3 +177,50 @@ def test_scenes_deterministic():
     assert d.materials["type"].tolist() == [0, 0, 0, 0]
     assert d.materials["emissionStrength"][2] == 0.0
     assert d.materials["ior"][0] == np.float32(1.5) and d.materials["absorptionStrength"].tolist() == [1, 1, 1, 1]
+
+
+# ---- optional binned-SAH builder ----------------------------------------------------
+def _check_bvh(b, ntri):
+    nodes = b.nodes
+    seen = np.zeros(ntri, np.int32)
+    depth_max = 0
+    stack = [(0, 1)]
+    while stack:
+        i, d = stack.pop()
+        depth_max = max(depth_max, d)
+        n = nodes[i]
+        lo, hi = n["min"], n["max"]
+        if n["triangleCount"] == 0:
+            left = int(n["leftNodeOrTriangleIndex"])
+            assert left % 2 == 1 and left + 1 < nodes.size          # children are a consecutive (odd, even) pair
+            for c in (left, left + 1):
+                assert np.all(nodes[c]["min"] >= lo) and np.all(nodes[c]["max"] <= hi)
+                stack.append((c, d + 1))
+        else:
+            first, cnt = int(n["leftNodeOrTriangleIndex"]), int(n["triangleCount"])
+            assert first % 3 == 0 and cnt % 3 == 0
+            v = b.positions[b.indices[first:first + cnt]]
+            assert np.all(v >= lo) and np.all(v <= hi)
+            assert np.array_equal(v.min(axis=0), lo) and np.array_equal(v.max(axis=0), hi)
+            seen[first // 3:(first + cnt) // 3] += 1
+    assert np.all(seen == 1)                                         # every triangle in exactly one leaf
+    return depth_max
+
+
+@pytest.mark.parametrize("name", ["cornell", "atrium"])
+def test_sah_bvh_valid_and_same_triangles(name):
+    s = wscene.generate(name)
+    m = s.meshes[0]
+    mesh = wscene.HostMesh(m.positions, m.indices)
+    sah = wscene.bvh_build(mesh, "sah")
+    ntri = m.indices.size // 3
+    depth = _check_bvh(sah, ntri)
+    assert depth <= 41
+    # same multiset of triangles as the input
+    assert np.array_equal(np.sort(m.indices.reshape(-1, 3).view("u4,u4,u4"), axis=0),
+                          np.sort(sah.indices.reshape(-1, 3).view("u4,u4,u4"), axis=0))
+    if name == "atrium":
+        mid = s.meshes[0]
+        leaves_sah = int((sah.nodes["triangleCount"] > 0).sum())
+        assert sah.nodes["triangleCount"].max() <= 3 * 8 or leaves_sah > 0
+        assert mid.nodes["triangleCount"].max() >= sah.nodes["triangleCount"].max()

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/wcpt.h"
@@ -179,6 +180,150 @@ int obj_parse(const char* text, uint64_t length, wcpt_mesh* out)
     }
     if (!outPos.empty()) memcpy(out->positions, outPos.data(), outPos.size() * sizeof(float));
     if (!outIdx.empty()) memcpy(out->indices, outIdx.data(), outIdx.size() * sizeof(uint32_t));
+    return WCPT_SUCCESS;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Binned SAH BVH (optional builder behind a flag). Same node format and numbering
+ * convention as the midpoint builder: root 0, children allocated as a consecutive pair when their parent splits,
+ * leaves = contiguous index-triple ranges, bounds = min/max over the leaf's vertices. The traversal kernels and the
+ * oracle consume it unchanged; only the tree differs (and with it the work), so images differ from the midpoint
+ * tree's only where two triangles hit at exactly the same t (the reference keeps the first one it tests).
+ * Split search: 16 centroid bins per axis, cost = 1 + (A_L N_L + A_R N_R) / A (traversal 1, triangle 1);
+ * a node becomes a leaf when no split beats its triangle count (up to kSahMaxLeaf triangles), at 1 triangle, or at
+ * kSahMaxDepth (the traversal stack holds 48 entries). Degenerate centroid extents fall back to an object median. */
+constexpr int kSahBins = 16;
+constexpr uint32_t kSahMaxLeaf = 8;   /* triangles */
+constexpr uint32_t kSahMaxDepth = 40;
+
+struct Aabb {
+    float lo[3], hi[3];
+    void reset() { for (int c = 0; c < 3; c++) { lo[c] = 3.40282347e38f; hi[c] = -3.40282347e38f; } }
+    void grow(const float* p) { for (int c = 0; c < 3; c++) { lo[c] = p[c] < lo[c] ? p[c] : lo[c]; hi[c] = p[c] > hi[c] ? p[c] : hi[c]; } }
+    void grow(const Aabb& b) { for (int c = 0; c < 3; c++) { lo[c] = b.lo[c] < lo[c] ? b.lo[c] : lo[c]; hi[c] = b.hi[c] > hi[c] ? b.hi[c] : hi[c]; } }
+    double area() const
+    {
+        if (hi[0] < lo[0]) return 0.0;
+        const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return 2.0 * (x * y + y * z + z * x);
+    }
+};
+
+int bvh_build_sah(const float* pos, uint32_t* idx, uint32_t index_count, wcpt_node* nodes, uint32_t max_nodes,
+                  uint32_t* nodes_used)
+{
+    const uint32_t ntri = index_count / 3;
+    std::vector<Aabb> tb(ntri);
+    std::vector<float> cen(3ull * ntri);
+    for (uint32_t t = 0; t < ntri; t++) {
+        tb[t].reset();
+        for (int v = 0; v < 3; v++) tb[t].grow(pos + 3ull * idx[3ull * t + v]);
+        for (int c = 0; c < 3; c++) cen[3ull * t + c] = 0.5f * (tb[t].lo[c] + tb[t].hi[c]);
+    }
+    /* work on a triangle permutation, then rewrite the index buffer in leaf order at the end */
+    std::vector<uint32_t> perm(ntri);
+    for (uint32_t t = 0; t < ntri; t++) perm[t] = t;
+    struct Work { uint32_t node, first, count, depth; };
+    std::vector<Work> stack;
+    uint32_t used = 1;
+    stack.push_back({0, 0, ntri, 0});
+    std::vector<uint32_t> tmp;
+    while (!stack.empty()) {
+        const Work w = stack.back();
+        stack.pop_back();
+        wcpt_node& node = nodes[w.node];
+        Aabb box, cbox;
+        box.reset();
+        cbox.reset();
+        for (uint32_t k = w.first; k < w.first + w.count; k++) {
+            box.grow(tb[perm[k]]);
+            cbox.grow(&cen[3ull * perm[k]]);
+        }
+        for (int c = 0; c < 3; c++) {
+            node.min[c] = box.lo[c];
+            node.max[c] = box.hi[c];
+        }
+        node.leftNodeOrTriangleIndex = 3u * w.first;
+        node.triangleCount = 3u * w.count;
+        if (w.count <= 1 || w.depth >= kSahMaxDepth) continue;
+        /* best binned split over the three axes */
+        double best = 1e300;
+        int best_axis = -1, best_bin = -1;
+        const double parent_area = box.area();
+        for (int a = 0; a < 3; a++) {
+            const float ext = cbox.hi[a] - cbox.lo[a];
+            if (!(ext > 0.0f)) continue;
+            Aabb bb[kSahBins];
+            uint32_t bn[kSahBins] = {};
+            for (int b = 0; b < kSahBins; b++) bb[b].reset();
+            const float scale = (float)kSahBins / ext;
+            for (uint32_t k = w.first; k < w.first + w.count; k++) {
+                int b = (int)((cen[3ull * perm[k] + a] - cbox.lo[a]) * scale);
+                b = b < 0 ? 0 : (b >= kSahBins ? kSahBins - 1 : b);
+                bb[b].grow(tb[perm[k]]);
+                bn[b]++;
+            }
+            double right_area[kSahBins];
+            uint32_t right_n[kSahBins];
+            Aabb acc;
+            acc.reset();
+            uint32_t n = 0;
+            for (int b = kSahBins - 1; b > 0; b--) {
+                acc.grow(bb[b]);
+                n += bn[b];
+                right_area[b] = acc.area();
+                right_n[b] = n;
+            }
+            acc.reset();
+            n = 0;
+            for (int b = 0; b < kSahBins - 1; b++) {
+                acc.grow(bb[b]);
+                n += bn[b];
+                if (n == 0 || right_n[b + 1] == 0) continue;
+                const double cost = acc.area() * n + right_area[b + 1] * right_n[b + 1];
+                if (cost < best) {
+                    best = cost;
+                    best_axis = a;
+                    best_bin = b;
+                }
+            }
+        }
+        uint32_t left_n = 0;
+        if (best_axis >= 0) {
+            const double split_cost = 1.0 + best / (parent_area > 0.0 ? parent_area : 1.0);
+            if (split_cost >= (double)w.count && w.count <= kSahMaxLeaf) continue; /* leaf is cheaper */
+            const float ext = cbox.hi[best_axis] - cbox.lo[best_axis];
+            const float scale = (float)kSahBins / ext;
+            auto in_left = [&](uint32_t t) {
+                int b = (int)((cen[3ull * t + best_axis] - cbox.lo[best_axis]) * scale);
+                b = b < 0 ? 0 : (b >= kSahBins ? kSahBins - 1 : b);
+                return b <= best_bin;
+            };
+            uint32_t* beg = perm.data() + w.first;
+            left_n = (uint32_t)(std::stable_partition(beg, beg + w.count, in_left) - beg);
+        }
+        if (left_n == 0 || left_n == w.count) {
+            if (w.count <= kSahMaxLeaf) continue;
+            /* all centroids in one bin: object median along the longest centroid axis */
+            int a = 0;
+            for (int c = 1; c < 3; c++)
+                if (cbox.hi[c] - cbox.lo[c] > cbox.hi[a] - cbox.lo[a]) a = c;
+            uint32_t* beg = perm.data() + w.first;
+            std::stable_sort(beg, beg + w.count, [&](uint32_t x, uint32_t y) { return cen[3ull * x + a] < cen[3ull * y + a]; });
+            left_n = w.count / 2;
+        }
+        if (used + 2 > max_nodes) return WCPT_ERROR_OUT_OF_HOST_MEMORY;
+        const uint32_t L = used++, R = used++;
+        node.leftNodeOrTriangleIndex = L;
+        node.triangleCount = 0;
+        stack.push_back({R, w.first + left_n, w.count - left_n, w.depth + 1});
+        stack.push_back({L, w.first, left_n, w.depth + 1});
+    }
+    /* index buffer in leaf order */
+    tmp.assign(idx, idx + index_count);
+    for (uint32_t k = 0; k < ntri; k++)
+        for (int v = 0; v < 3; v++) idx[3ull * k + v] = tmp[3ull * perm[k] + v];
+    *nodes_used = used;
     return WCPT_SUCCESS;
 }
 
@@ -725,6 +870,20 @@ int wcpt_bvh_build(const float* positions, uint32_t vertex_count, uint32_t* indi
         if (indices[i] >= vertex_count) return WCPT_ERROR_INVALID_ARGUMENT;
     try {
         return bvh_build(positions, indices, index_count, nodes, max_nodes, nodes_used);
+    } catch (...) {
+        return WCPT_ERROR_OUT_OF_HOST_MEMORY;
+    }
+}
+
+int wcpt_bvh_build_sah(const float* positions, uint32_t vertex_count, uint32_t* indices, uint32_t index_count,
+                       wcpt_node* nodes, uint32_t max_nodes, uint32_t* nodes_used)
+{
+    if (!positions || !indices || !nodes || !nodes_used || max_nodes < 1) return WCPT_ERROR_INVALID_ARGUMENT;
+    if (index_count == 0 || index_count % 3 != 0) return WCPT_ERROR_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < index_count; i++)
+        if (indices[i] >= vertex_count) return WCPT_ERROR_INVALID_ARGUMENT;
+    try {
+        return bvh_build_sah(positions, indices, index_count, nodes, max_nodes, nodes_used);
     } catch (...) {
         return WCPT_ERROR_OUT_OF_HOST_MEMORY;
     }

@@ -135,6 +135,7 @@ _PROTOTYPES = {
     "wcpt_obj_load": (_i, [C.c_char_p, C.POINTER(Mesh)]),
     "wcpt_mesh_free": (None, [C.POINTER(Mesh)]),
     "wcpt_bvh_build": (_i, [_p, _u32, _p, _u32, _p, _u32, C.POINTER(_u32)]),
+    "wcpt_bvh_build_sah": (_i, [_p, _u32, _p, _u32, _p, _u32, C.POINTER(_u32)]),
     "wcpt_camera_update": (_i, [C.POINTER(Camera), C.c_float]),
     "wcpt_scene_generate": (_i, [C.c_char_p, _u32, C.POINTER(SceneC)]),
     "wcpt_scene_free": (None, [C.POINTER(SceneC)]),

@@ -109,14 +109,18 @@ def mesh_to_obj(mesh: HostMesh) -> bytes:
         lib.wcpt_string_free(out)
 
 
-def bvh_build(mesh: HostMesh) -> HostBVH:
-    """Midpoint BVH (PathTracingRenderer.jai:147-217); returns the permuted index buffer with it."""
+def bvh_build(mesh: HostMesh, builder: str = "midpoint") -> HostBVH:
+    """Midpoint BVH (PathTracingRenderer.jai:147-217, the reference's) or, with builder="sah", the optional
+    binned-SAH builder; returns the permuted index buffer with it."""
+    if builder not in ("midpoint", "sah"):
+        raise ValueError(f"unknown BVH builder {builder!r}")
     pos = np.ascontiguousarray(mesh.positions, dtype=np.float32)
     idx = np.ascontiguousarray(mesh.indices, dtype=np.uint32).copy()
     max_nodes = max(1, 2 * (idx.size // 3))
     nodes = np.zeros(max_nodes, dtype=NODE_DTYPE)
     used = C.c_uint32()
-    check(lib.wcpt_bvh_build(ptr(pos), pos.shape[0], ptr(idx), idx.size, ptr(nodes), max_nodes, C.byref(used)))
+    fn = lib.wcpt_bvh_build if builder == "midpoint" else lib.wcpt_bvh_build_sah
+    check(fn(ptr(pos), pos.shape[0], ptr(idx), idx.size, ptr(nodes), max_nodes, C.byref(used)))
     return HostBVH(pos, idx, nodes[: used.value].copy())
 
 
@@ -134,7 +138,7 @@ def make_camera(position=(0.0, 0.0, 0.0), yaw=0.0, pitch=0.0, fov=90.0) -> Camer
     return c
 
 
-def generate(name: str, seed: int = 0, via_obj: bool = True) -> HostScene:
+def generate(name: str, seed: int = 0, via_obj: bool = True, bvh: str = "midpoint") -> HostScene:
     """Synthetic scene -> HostScene. With via_obj the mesh goes through OBJ text and the loader, like
     LoadModel's parse_obj_file (the atrium is the Sponza-scale OBJ of configs 3-5)."""
     s = SceneC()
@@ -153,7 +157,7 @@ def generate(name: str, seed: int = 0, via_obj: bool = True) -> HostScene:
     if mesh.indices.size:
         if via_obj:
             mesh = obj_parse(mesh_to_obj(mesh))
-        scene.meshes.append(bvh_build(mesh))
+        scene.meshes.append(bvh_build(mesh, bvh))
     return scene
 
 
