@@ -32,33 +32,37 @@ struct LaunchArgs {
 };
 
 /* Wavefront path state (pt_wavefront.hip): structure-of-arrays in one device allocation. */
+/* Path state indexed by queue slot (structure of arrays): the kernels that produce a queue write it compacted,
+ * in append order, so every consumer reads it with coalesced loads (no per-pixel gathers). */
+struct PathSoA {
+    float4* ray0;      /* (origin.xyz, direction.x)                                     */
+    float4* ray1;      /* (direction.yz, bounce bits, sample bits)                      */
+    float4* pre;       /* (invDirection.xyz, t of the sphere loop)                      */
+    float4* light;     /* (totalLight.xyz, rng state bits)                              */
+    float4* trans;     /* (transmittance.xyz, -)                                        */
+    uint32_t* pre_prim;/* sphere loop's winner (kSpherePrim | i) or kNoPrim             */
+    uint32_t* pix;     /* pixel index (ly * W + lx) of the path                         */
+};
 struct WfBuffers {
-    float4* ray0;      /* (origin.xyz, direction.x)                       */
-    float4* ray1;      /* (direction.yz, bounce bits, sample bits)        */
-    float4* light;     /* (totalLight.xyz, rng state bits)                */
-    float4* trans;     /* (transmittance.xyz, -)                          */
-    float4* result;    /* (sum of sample radiance .xyz, -)                */
-    float4* pre;       /* (invDirection.xyz, t of the sphere loop) of the queued ray          */
-    uint32_t* pre_prim;/* sphere loop's winner (kSpherePrim | i) or kNoPrim                  */
-    float4* hit;       /* (t, primitive bits, draw bits, -) of the last Intersect             */
-    uint32_t* queue_in;
+    PathSoA in;        /* queue being traced / shaded this iteration                    */
+    PathSoA out;       /* queue shade appends the continuing paths to                   */
+    float4* hit;       /* by input slot: (t, primitive bits, draw bits, -) of Intersect */
+    float4* result;    /* by pixel: sum of sample radiance .xyz                          */
+    const uint32_t* order; /* optional trace order of the input slots (ray sorting), or null */
     uint32_t* count_in;
-    uint32_t* queue_out;
     uint32_t* count_out;
-    uint32_t* head;    /* trace kernel's dequeue position                 */
-    unsigned long long* diag; /* DIAG builds: trace-loop phase timers (8 x u64) */
+    uint32_t* head;    /* trace kernel's dequeue position                               */
+    unsigned long long* diag; /* DIAG builds: trace-loop phase timers (8 x u64)         */
 };
 struct WfState {
     void* mem = nullptr;
     uint32_t capacity = 0;
-    float4 *ray0 = nullptr, *ray1 = nullptr, *light = nullptr, *trans = nullptr, *result = nullptr, *hit = nullptr;
-    float4* pre = nullptr;
-    uint32_t* pre_prim = nullptr;
-    uint32_t* queue[2] = {nullptr, nullptr};
+    PathSoA soa[2] = {};
+    float4 *hit = nullptr, *result = nullptr;
     uint32_t* ctr = nullptr;
     unsigned long long* diag = nullptr;
     void* sort_mem = nullptr;
-    uint32_t *sort_keys = nullptr, *sort_keys_alt = nullptr, *sort_vals = nullptr;
+    uint32_t *sort_keys = nullptr, *sort_keys_alt = nullptr, *sort_iota = nullptr, *sort_order = nullptr;
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
 };

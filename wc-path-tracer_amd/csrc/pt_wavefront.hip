@@ -41,17 +41,15 @@ constexpr int kShadeBlock = 256;
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
-/* Queue a ray for the next trace: its state plus the Intersect prologue (:136-149, the sphere loop) and
- * 1/direction, computed here with all lanes busy. Counts the segment (one Intersect call per queued ray). */
+/* The Intersect prologue of a new segment (:136-149, the sphere loop), run where the ray is created with every
+ * lane busy; its result travels with the ray in `pre`. Counts the segment (one Intersect call per queued ray). */
 template <bool COUNT>
-__device__ __forceinline__ void store_segment(const WfBuffers& b, uint32_t p, const Ray& r, uint32_t bounce,
-                                              uint32_t sample, const wcpt_scene_data& sd,
-                                              const wcpt_sphere* __restrict__ spheres, Counters& cnt)
+__device__ __forceinline__ void segment_prologue(const Ray& r, const wcpt_scene_data& sd,
+                                                 const wcpt_sphere* __restrict__ spheres, float& rt, uint32_t& prim,
+                                                 Counters& cnt)
 {
-    b.ray0[p] = make_float4(r.origin.x, r.origin.y, r.origin.z, r.direction.x);
-    b.ray1[p] = make_float4(r.direction.y, r.direction.z, __uint_as_float(bounce), __uint_as_float(sample));
-    float rt = kInfinity;
-    uint32_t prim = kNoPrim;
+    rt = kInfinity;
+    prim = kNoPrim;
     for (uint32_t i = 0; i < sd.sphereCount; i++) {
         const wcpt_sphere& s = spheres[i];
         const float tempRec = raySphereNear(r, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
@@ -64,8 +62,20 @@ __device__ __forceinline__ void store_segment(const WfBuffers& b, uint32_t p, co
         cnt.segments++;
         cnt.sphere_tests += sd.sphereCount;
     }
-    b.pre[p] = make_float4(r.invDirection.x, r.invDirection.y, r.invDirection.z, rt);
-    b.pre_prim[p] = prim;
+}
+
+/* Write one queued path at `slot` of a slot-indexed state set. */
+__device__ __forceinline__ void write_path(const PathSoA& o, uint32_t slot, const Ray& r, uint32_t bounce,
+                                           uint32_t sample, float rt, uint32_t prim, f3 light, uint32_t seed, f3 trans,
+                                           uint32_t pix)
+{
+    o.ray0[slot] = make_float4(r.origin.x, r.origin.y, r.origin.z, r.direction.x);
+    o.ray1[slot] = make_float4(r.direction.y, r.direction.z, __uint_as_float(bounce), __uint_as_float(sample));
+    o.pre[slot] = make_float4(r.invDirection.x, r.invDirection.y, r.invDirection.z, rt);
+    o.light[slot] = make_float4(light.x, light.y, light.z, __uint_as_float(seed));
+    o.trans[slot] = make_float4(trans.x, trans.y, trans.z, 0.0f);
+    o.pre_prim[slot] = prim;
+    o.pix[slot] = pix;
 }
 
 /* Block-aggregated append of `pred` lanes to a queue: one atomicAdd per block. All threads of the block must
@@ -104,7 +114,9 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
         const uint32_t w = base + threadIdx.x;
         bool live = false;
-        uint32_t p = 0;
+        uint32_t p = 0, seed = 0, prim = kNoPrim;
+        float rt = kInfinity;
+        Ray ray;
         if (w < total) {
             const uint32_t t = w >> 6, q = w & 63u;           /* 8x8 tiles: coherent initial queue */
             const uint32_t lx = (t % tilesX) * 8u + (q & 7u);
@@ -112,15 +124,14 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
             if (lx < W && ly < rows) {
                 p = ly * W + lx;
                 const uint32_t y = y0 + ly;
-                const uint32_t seed = pcg_hash(lx + y * W + sd.renderedFramesCount * 719393u); /* :304-305 */
+                seed = pcg_hash(lx + y * W + sd.renderedFramesCount * 719393u); /* :304-305 */
                 b.result[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 if (sd.samples > 0) {
                     PathState ps;
                     path_begin(ps, mk3(sd.position[0], sd.position[1], sd.position[2]),
                                primary_direction(sd, lx, y, W, H));
-                    store_segment<COUNT>(b, p, ps.ray, 0u, 0u, sd, spheres, cnt);
-                    b.light[p] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(seed));
-                    b.trans[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+                    ray = ps.ray;
+                    segment_prologue<COUNT>(ray, sd, spheres, rt, prim, cnt);
                     live = true;
                 } else { /* samples == 0: result / 0 = NaN (:312), stored as the reference would */
                     const f3 r = mk3(0.0f, 0.0f, 0.0f) / (float)sd.samples;
@@ -130,7 +141,8 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
             }
         }
         const uint32_t slot = block_append(b.count_in, live, s_wave, &s_base);
-        if (live) b.queue_in[slot] = p;
+        if (live)
+            write_path(b.in, slot, ray, 0u, 0u, rt, prim, mk3(0.0f, 0.0f, 0.0f), seed, mk3(1.0f, 1.0f, 1.0f), p);
     }
     flush_counters<COUNT>(cnt, counters);
 }
@@ -263,13 +275,15 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 const uint32_t rank = (uint32_t)__popcll(need & lanemask_lt());
                 const bool take = ((need >> lane) & 1ull) && rank < avail;
                 if (take) {
-                    p = b.queue_in[lo + rank];
-                    const float4 r0 = b.ray0[p], r1 = b.ray1[p], pr = b.pre[p];
+                    p = b.order ? b.order[lo + rank] : lo + rank;   /* input slot: consecutive lanes, consecutive slots */
+                    const float4 r0 = b.in.ray0[p];
+                    const float2 r1 = reinterpret_cast<const float2*>(b.in.ray1)[2u * p];
+                    const float4 pr = b.in.pre[p];
                     ray.origin = mk3(r0.x, r0.y, r0.z);
                     ray.direction = mk3(r0.w, r1.x, r1.y);
                     ray.invDirection = mk3(pr.x, pr.y, pr.z);
                     rt = pr.w;                /* sphere loop (:136-149), run by the ray's creator */
-                    prim = b.pre_prim[p];
+                    prim = b.in.pre_prim[p];
                     if (COUNT) simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
                     d = 0;
                     start_draw();
@@ -384,18 +398,20 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t w = base + threadIdx.x;
         bool cont = false;
-        uint32_t p = 0;
+        uint32_t p = 0, sample = 0, seed = 0, prim0 = kNoPrim;
+        float rt0 = kInfinity;
+        PathState ps;
         if (w < n) {
-            p = b.queue_in[w];
-            const float4 r0 = b.ray0[p], r1 = b.ray1[p], li = b.light[p], tr = b.trans[p], hi = b.hit[p];
-            PathState ps;
+            p = b.in.pix[w];                     /* slot w of the compacted input queue */
+            const float4 r0 = b.in.ray0[w], r1 = b.in.ray1[w], li = b.in.light[w], tr = b.in.trans[w];
+            const float4 hi = b.hit[w];
             ps.ray.origin = mk3(r0.x, r0.y, r0.z);
             ps.ray.direction = mk3(r0.w, r1.x, r1.y);
             ps.totalLight = mk3(li.x, li.y, li.z);
             ps.transmittance = mk3(tr.x, tr.y, tr.z);
             ps.bounce = __float_as_uint(r1.z);
-            uint32_t sample = __float_as_uint(r1.w);
-            uint32_t seed = __float_as_uint(li.w);
+            sample = __float_as_uint(r1.w);
+            seed = __float_as_uint(li.w);
             const uint32_t prim = __float_as_uint(hi.y);
             const Hit h = resolve_hit(ps.ray, hi.x, prim, __float_as_uint(hi.z), spheres, draws);
             if (COUNT && h.hit) cnt.hits++;
@@ -431,14 +447,11 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
                     if (COUNT) cnt.pixels++;
                 }
             }
-            if (cont) {
-                store_segment<COUNT>(b, p, ps.ray, ps.bounce, sample, sd, spheres, cnt);
-                b.light[p] = make_float4(ps.totalLight.x, ps.totalLight.y, ps.totalLight.z, __uint_as_float(seed));
-                b.trans[p] = make_float4(ps.transmittance.x, ps.transmittance.y, ps.transmittance.z, 0.0f);
-            }
+            if (cont) segment_prologue<COUNT>(ps.ray, sd, spheres, rt0, prim0, cnt);
         }
         const uint32_t slot = block_append(b.count_out, cont, s_wave, &s_base);
-        if (cont) b.queue_out[slot] = p;
+        if (cont)
+            write_path(b.out, slot, ps.ray, ps.bounce, sample, rt0, prim0, ps.totalLight, seed, ps.transmittance, p);
     }
     flush_counters<COUNT>(cnt, counters);
 }
@@ -465,38 +478,48 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     if (paths <= s.capacity) return hipSuccess;
     wf_release(s);
     const size_t P = paths;
-    const size_t bytes = P * (7 * sizeof(float4) + 3 * sizeof(uint32_t)) + 256;
+    /* two slot-indexed state sets (5 float4 + 2 u32 arrays each), the hit records, the per-pixel sample sums,
+     * then the counters and the diagnostics block */
+    const size_t bytes = P * (2 * (5 * sizeof(float4) + 2 * sizeof(uint32_t)) + 2 * sizeof(float4)) + 256;
     char* m = nullptr;
     hipError_t e = hipMalloc(&m, bytes);
     if (e != hipSuccess) return e;
     s.mem = m;
     float4* f = reinterpret_cast<float4*>(m);
-    s.ray0 = f;
-    s.ray1 = f + P;
-    s.light = f + 2 * P;
-    s.trans = f + 3 * P;
-    s.result = f + 4 * P;
-    s.hit = f + 5 * P;
-    s.pre = f + 6 * P;
-    s.pre_prim = reinterpret_cast<uint32_t*>(f + 7 * P);
-    s.queue[0] = s.pre_prim + P;
-    s.queue[1] = s.queue[0] + P;
-    s.ctr = s.queue[1] + P; /* [0] count q0, [1] count q1, [2] trace head */
+    for (int k = 0; k < 2; k++) {
+        PathSoA& o = s.soa[k];
+        o.ray0 = f;
+        o.ray1 = f + P;
+        o.pre = f + 2 * P;
+        o.light = f + 3 * P;
+        o.trans = f + 4 * P;
+        f += 5 * P;
+    }
+    s.hit = f;
+    s.result = f + P;
+    uint32_t* u = reinterpret_cast<uint32_t*>(f + 2 * P);
+    for (int k = 0; k < 2; k++) {
+        s.soa[k].pre_prim = u;
+        s.soa[k].pix = u + P;
+        u += 2 * P;
+    }
+    s.ctr = u; /* [0] count q0, [1] count q1, [2] trace head */
     s.diag = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(s.ctr + 4 + 7) & ~uintptr_t(7));
     s.capacity = paths;
-    /* ray-sort scratch: keys, alternate keys, sorted queue, radix-sort temporary storage */
+    /* ray-sort scratch: keys, alternate keys, slot ids, sorted order, radix-sort temporary storage */
     size_t temp = 0;
     e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)paths, 0, 32);
     if (e != hipSuccess) return e;
     char* q = nullptr;
-    e = hipMalloc(&q, 3 * P * sizeof(uint32_t) + temp + 256);
+    e = hipMalloc(&q, 4 * P * sizeof(uint32_t) + temp + 256);
     if (e != hipSuccess) return e;
     s.sort_mem = q;
     s.sort_keys = reinterpret_cast<uint32_t*>(q);
     s.sort_keys_alt = s.sort_keys + P;
-    s.sort_vals = s.sort_keys_alt + P;
-    s.sort_temp = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(s.sort_vals + P) + 255) & ~uintptr_t(255));
+    s.sort_iota = s.sort_keys_alt + P;
+    s.sort_order = s.sort_iota + P;
+    s.sort_temp = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(s.sort_order + P) + 255) & ~uintptr_t(255));
     s.sort_temp_bytes = temp;
     return hipSuccess;
 }
@@ -524,7 +547,7 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v)
 }
 
 __global__ __launch_bounds__(256) void wf_sort_keys(WfBuffers b, uint32_t P, const wcpt_draw_command* __restrict__ draws,
-                                                    uint32_t* __restrict__ keys)
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ iota)
 {
     const uint32_t n = *b.count_in;
     const dev::gnode_ptr root = dev::as_nodes(draws[0].bvhBuffer);
@@ -533,8 +556,7 @@ __global__ __launch_bounds__(256) void wf_sort_keys(WfBuffers b, uint32_t P, con
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
         uint32_t key = 0xFFFFFFFFu;
         if (i < n) {
-            const uint32_t p = b.queue_in[i];
-            const float4 r0 = b.ray0[p], r1 = b.ray1[p];
+            const float4 r0 = b.in.ray0[i], r1 = b.in.ray1[i];
             const float o[3] = {r0.x, r0.y, r0.z};
             const uint32_t oct = (r0.w < 0.0f ? 4u : 0u) | (r1.x < 0.0f ? 2u : 0u) | (r1.y < 0.0f ? 1u : 0u);
             uint32_t m = 0;
@@ -547,6 +569,7 @@ __global__ __launch_bounds__(256) void wf_sort_keys(WfBuffers b, uint32_t P, con
             key = (oct << 27) | m;
         }
         keys[i] = key;
+        iota[i] = i;
     }
 }
 
@@ -593,14 +616,13 @@ static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b
                              hipStream_t stream)
 {
     const uint32_t grid = min((P + 255u) / 256u, (uint32_t)cus * 8u);
-    hipLaunchKernelGGL(wf_sort_keys, dim3(grid), dim3(256), 0, stream, b, P, a.draws, s.sort_keys);
+    hipLaunchKernelGGL(wf_sort_keys, dim3(grid), dim3(256), 0, stream, b, P, a.draws, s.sort_keys, s.sort_iota);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t temp = s.sort_temp_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(s.sort_temp, temp, s.sort_keys, s.sort_keys_alt, b.queue_in, s.sort_vals,
-                                           (int)P, 0, 32, stream);
-    if (e != hipSuccess) return e;
-    return hipMemcpyAsync(b.queue_in, s.sort_vals, (size_t)P * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
+    /* values: slot ids 0..P-1 -> the trace order of the input slots (b.order) */
+    return hipcub::DeviceRadixSort::SortPairs(s.sort_temp, temp, s.sort_keys, s.sort_keys_alt, s.sort_iota,
+                                              s.sort_order, (int)P, 0, 32, stream);
 }
 
 hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, int lds_stack, hipStream_t stream)
@@ -633,14 +655,19 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     e = hipMemsetAsync(s.ctr, 0, 4 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     WfBuffers b;
-    b.ray0 = s.ray0; b.ray1 = s.ray1; b.light = s.light; b.trans = s.trans; b.result = s.result;
-    b.hit = s.hit; b.pre = s.pre; b.pre_prim = s.pre_prim; b.head = s.ctr + 2; b.diag = s.diag;
+    b.in = s.soa[0];
+    b.out = s.soa[1];
+    b.result = s.result;
+    b.hit = s.hit;
+    b.order = nullptr;
+    b.head = s.ctr + 2;
+    b.diag = s.diag;
     if (mode == kModeDiag) {
         e = hipMemsetAsync(s.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
     }
-    b.queue_in = s.queue[0]; b.count_in = s.ctr + 0;
-    b.queue_out = s.queue[1]; b.count_out = s.ctr + 1;
+    b.count_in = s.ctr + 0;
+    b.count_out = s.ctr + 1;
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);
     if (count)
         hipLaunchKernelGGL(dev::wf_init<true>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
@@ -655,14 +682,16 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     if (iters > (1ull << 20)) iters = 1ull << 20; /* bounded; WCPT documents the cap */
     sort_rays = sort_rays && a.sd.drawCommandCount > 0;
     for (uint64_t it = 0; it < iters; it++) {
+        b.order = nullptr;
         if (sort_rays && it > 0) { /* bounce rays; the primary queue is already in 8x8-tile order */
             e = sort_queue(a, s, b, P, cus, stream);
             if (e != hipSuccess) return e;
+            b.order = s.sort_order;
         }
         int unused = 0;
         e = wf_dispatch(mode, single, ldsn, false, unused, a, b, trace_grid, shade_grid, stream);
         if (e != hipSuccess) return e;
-        std::swap(b.queue_in, b.queue_out);
+        std::swap(b.in, b.out);
         std::swap(b.count_in, b.count_out);
     }
     return hipSuccess;
