@@ -275,7 +275,11 @@ def main():
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                         "note": ("algorithmic bytes price every scene fetch at HBM cost (SURVEY 8(d)); the scene is "
+                                  "cache-resident, so frac can exceed 1 and 'traffic' (PMC HBM bytes) is the real "
+                                  "HBM load; the binding resource is VALU issue (c1/c2) or dependent-fetch latency "
+                                  "(c3/c4), DESIGN.md section 3")},
         }
         if verified is not None:
             out["verified"] = verified
