@@ -65,6 +65,8 @@ struct WfState {
     uint32_t *sort_keys = nullptr, *sort_keys_alt = nullptr, *sort_iota = nullptr, *sort_order = nullptr;
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
+    int cus = 0;                   /* compute units of the context's device (0 = not yet queried)          */
+    int trace_bpc[3][2][3] = {};   /* trace-kernel blocks per CU by (mode, single draw, LDS stack variant)  */
 };
 
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD

@@ -459,17 +459,17 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
 } // namespace dev
 
 /* ---------------------------------------------------------------------------------------------------- */
-static int g_cus = 0;
-
-static hipError_t cu_count(int& cus)
+/* CU count of the current device, cached per context (WfState) so that contexts on different devices each use
+ * their own. */
+static hipError_t cu_count(WfState& s, int& cus)
 {
-    if (g_cus == 0) {
+    if (s.cus == 0) {
         int dev = 0;
         hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
     }
-    cus = g_cus;
+    cus = s.cus;
     return hipSuccess;
 }
 
@@ -637,13 +637,12 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     hipError_t e = wf_reserve(s, P);
     if (e != hipSuccess) return e;
     int cus = 0;
-    e = cu_count(cus);
+    e = cu_count(s, cus);
     if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
     const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
     const int ldsn = (lds_stack == 16 || lds_stack == 24) ? lds_stack : 10;
-    static int trace_bpc[3][2][3] = {};
-    int& bpc = trace_bpc[mode][single ? 1 : 0][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
+    int& bpc = s.trace_bpc[mode][single ? 1 : 0][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
     if (bpc == 0) {
         e = wf_dispatch(mode, single, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);
         if (e != hipSuccess) return e;
