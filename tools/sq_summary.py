@@ -1,0 +1,51 @@
+"""Summarise rocprofv3 SQ/TCC counter passes (tools/pmc_one.sh) for the dominant render kernel of a config.
+
+    python tools/sq_summary.py gpurun_out/sq_c2/pmc --kernel "pt_megakernel<false" --cycles-per-sec 2.4e9 \
+        --ms 0.59 [--json out.json]
+
+Derived: VALU issue share = SQ_INSTS_VALU * 4 cycles / (SIMDs * kernel cycles) (MI355X_MICROARCH.md: 4 cycles per
+wave64 VALU instruction per SIMD); wave-cycle split (WAIT_ANY / WAIT_INST_ANY / ACTIVE_INST_ANY over WAVE_CYCLES);
+L2 hit rate = TCC_HIT / (TCC_HIT + TCC_MISS).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--launches-per-frame", type=float, default=1.0)
+    ap.add_argument("--ms", type=float, required=True, help="average duration of one launch of the kernel")
+    ap.add_argument("--cycles-per-sec", type=float, default=2.4e9)
+    ap.add_argument("--simds", type=int, default=1024)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(a.dir, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if a.kernel in row.get("Kernel_Name", ""):
+                per[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    m = {k: sum(v) / len(v) for k, v in per.items()}
+    out = {"kernel": a.kernel, "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())}}
+    cycles = a.ms * 1e-3 * a.cycles_per_sec
+    if "SQ_INSTS_VALU" in m:
+        out["valu_issue_share"] = round(m["SQ_INSTS_VALU"] * 4.0 / (a.simds * cycles), 3)
+    if "SQ_WAVE_CYCLES" in m:
+        w = m["SQ_WAVE_CYCLES"]
+        out["wave_cycle_split"] = {k: round(m[c] / w, 3) for k, c in
+                                   (("wait_any", "SQ_WAIT_ANY"), ("wait_inst_any", "SQ_WAIT_INST_ANY"),
+                                    ("active_inst_any", "SQ_ACTIVE_INST_ANY")) if c in m}
+    if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
+        out["l2_hit_rate"] = round(m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 3)
+    print(json.dumps(out, indent=1))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
