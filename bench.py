@@ -38,6 +38,8 @@ CONFIGS = {
     "c4": ("atrium", 3840, 2160, 16, 4, "Sponza-scale atrium OBJ (262k tris), 3840x2160, 16 spp, 4 bounces"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BASELINE_METRIC = "Mray/s + ms/frame at 1920\u00d71080 1spp; achieved HBM GB/s vs peak"  # BASELINE.json "metric"
+# rays = ray segments (Intersect() calls), counted exactly by the instrumented kernel
 # Measured best kernel per workload: the megakernel wins on the coherent, L1-resident
 # Cornell box; the wavefront variant wins on the 262k-triangle atrium (incoherent, MALL-resident).
 DEFAULT_KERNEL = {"c1": wcpt.KERNEL_MEGAKERNEL, "c2": wcpt.KERNEL_MEGAKERNEL, "c3": wcpt.KERNEL_WAVEFRONT,
@@ -251,7 +253,7 @@ def main():
             except Exception:
                 traffic = None
         out = {
-            "metric": "Mray/s (ray segments) + ms/frame at 1920x1080 1spp; achieved HBM GB/s vs peak",
+            "metric": BASELINE_METRIC,
             "value": round(value, 3),
             "unit": "Mray/s",
             "n_gpus": world,
