@@ -649,7 +649,16 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
         if (bpc < 1) bpc = 1;
     }
     const uint32_t trace_grid = (uint32_t)(bpc * cus);
-    const uint32_t shade_grid = (uint32_t)(cus * 8);
+/* Shade blocks per CU (grid-stride over the queue). The continuing paths are appended in roughly the order
+ * the blocks walk their chunks, so a small grid keeps the next queue close to the input order (coherent rays
+ * for the next trace). Measured on c3: 4 -> 7.98 ms, 8 -> 8.13, 16 -> 8.56, 32 -> 8.98, one thread per slot ->
+ * 8.97. */
+#ifndef WCPT_SHADE_BLOCKS_PER_CU
+#define WCPT_SHADE_BLOCKS_PER_CU 4
+#endif
+    /* 0: one thread per path slot (no grid-stride loop) */
+    const uint32_t shade_grid = WCPT_SHADE_BLOCKS_PER_CU > 0 ? (uint32_t)(cus * WCPT_SHADE_BLOCKS_PER_CU)
+                                                             : (P + dev::kShadeBlock - 1) / dev::kShadeBlock;
 
     e = hipMemsetAsync(s.ctr, 0, 4 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
