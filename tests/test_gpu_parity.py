@@ -573,3 +573,50 @@ def test_sah_bvh_frames(gpu_ctx, kernel):
     assert differ <= 0.01, f"{differ:.4f} of pixels differ between SAH and midpoint trees"
     assert cnt["segments"] == cnt_mid["segments"] or differ > 0
     assert cnt["interior_visits"] < cnt_mid["interior_visits"]
+
+
+# ---- randomized scenes ------------------------------------------------------------------------------------
+def _random_scene(seed):
+    """Random materials (metal and dielectric, emissive, rough), spheres (overlapping, camera possibly inside
+    one), 1-2 triangle meshes of random size with the midpoint BVH, and a random camera."""
+    rng = np.random.default_rng(seed)
+    nm = int(rng.integers(1, 6))
+    mats = np.zeros(nm, dtype=wcpt.MATERIAL_DTYPE)
+    mats["type"] = rng.integers(0, 2, nm)
+    mats["albedo"] = rng.random((nm, 3))
+    mats["emission"] = rng.random((nm, 3))
+    mats["emissionStrength"] = rng.random(nm) * rng.integers(0, 2, nm) * 4.0
+    mats["roughness"] = rng.random(nm) * rng.integers(0, 2, nm)
+    mats["absorption"] = rng.random((nm, 3))
+    mats["absorptionStrength"] = rng.random(nm) * 2.0
+    mats["ior"] = 1.0 + rng.random(nm) * 1.5
+    ns = int(rng.integers(0, 7))
+    sph = np.zeros(ns, dtype=wcpt.SPHERE_DTYPE)
+    sph["position"] = (rng.random((ns, 3)) * 6.0 - 3.0).astype(np.float32)
+    sph["radius"] = (0.2 + rng.random(ns) * 1.5).astype(np.float32)
+    sph["material"] = rng.integers(0, nm, ns)
+    meshes = []
+    for _ in range(int(rng.integers(0, 3))):
+        nt = int(rng.integers(1, 400))
+        centers = rng.random((nt, 1, 3)) * 6.0 - 3.0
+        pos = (centers + (rng.random((nt, 3, 3)) - 0.5) * rng.random() * 2.0).reshape(-1, 3).astype(np.float32)
+        idx = np.arange(nt * 3, dtype=np.uint32)
+        rng.shuffle(idx.reshape(-1, 3))
+        meshes.append(wscene.bvh_build(wscene.HostMesh(pos, idx)))
+    cam = wscene.make_camera(position=tuple((rng.random(3) * 6.0 - 3.0).tolist()), yaw=float(rng.random() * 360.0),
+                             pitch=float(rng.random() * 120.0 - 60.0), fov=float(30.0 + rng.random() * 90.0))
+    s = wscene.HostScene(f"random{seed}", mats, sph, cam)
+    s.meshes = meshes
+    return s, int(rng.integers(0, 7)), int(rng.integers(1, 4)), int(rng.integers(0, 50))
+
+
+@pytest.mark.parametrize("seed", list(range(12)))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_random_scenes_match_oracle(gpu_ctx, seed, kernel):
+    s, bounces, spp, frame = _random_scene(seed)
+    W, H = 40, 28
+    init = np.random.default_rng(seed + 100).random((H, W, 4)).astype(np.float32)
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, init=init, kernel=kernel)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, image=init, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
