@@ -211,7 +211,9 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { r
 /* Derived triangle records. For each draw command the runtime derives from the draw's index and vertex buffers,
  * triangle k = index positions 3k..3k+2, with e1 = b - a and e2 = c - a computed by the same binary32
  * subtractions as :122-123, two record arrays:
- *   single records, 48 B per triangle: (a.xyz, e1.x) (e1.yz, e2.xy) (e2.z, 0, 0, 0);
+ *   single records, 48 B per triangle: (a.xyz, e1.x) (e1.yz, e2.xy) (e2.z, n.xyz), where n = normalize(cross(e1,
+ *     e2)) is the geometric normal of :173 evaluated once per triangle with the same operations (it depends on
+ *     the triangle only), so the hit epilogue reads it instead of re-gathering three indices and vertices;
  *   pair records, 80 B per triangle pair (2j, 2j+1): the nine components of both triangles as float2
  *     {tri 2j, tri 2j+1} + 8 B pad. One lane then tests two triangles at once with packed-FP32 instructions
  *     (v_pk_mul_f32 / v_pk_add_f32 perform two independent binary32 ops each -- exactly the reference's ops),
@@ -397,11 +399,32 @@ struct LdsStack {
  * computes at each update (:145, :173) without paying a normalize per closer hit. */
 constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
+/* Geometric normal of the triangle at index positions prim..prim+2 of draw `draw` (:173): from its single record
+ * when the triangle starts on a triangle boundary inside the records (the record was derived from exactly these
+ * three indices), else recomputed from the index and vertex buffers with the same expression. */
+__device__ __forceinline__ f3 triangle_normal(uint32_t prim, uint32_t draw, const wcpt_draw_command* __restrict__ draws,
+                                              const uint64_t* __restrict__ tri_records)
+{
+    const uint32_t k = prim / 3u;
+    if (tri_records && k * 3u == prim && k < (uint32_t)tri_records[kTriTableWords * draw + 2u]) {
+        const gtri_ptr t = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * draw];
+        const v4f r2 = t[3ull * k + 2u];
+        return mk3(r2.y, r2.z, r2.w);
+    }
+    const gu32_ptr idx = as_u32(draws[draw].indexBuffer);
+    const gf32_ptr vtx = as_f32(draws[draw].vertexBuffer);
+    const f3 a = ld3(vtx + 3ull * idx[prim + 0]);
+    const f3 b = ld3(vtx + 3ull * idx[prim + 1]);
+    const f3 c = ld3(vtx + 3ull * idx[prim + 2]);
+    return normalize(cross(b - a, c - a));
+}
+
 /* Intersect epilogue (:204-208) for winner `prim` (kNoPrim, kSpherePrim | sphere, or the index position of
  * a triangle of draw `draw`) at distance t. */
 __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t prim, uint32_t draw,
                                            const wcpt_sphere* __restrict__ spheres,
-                                           const wcpt_draw_command* __restrict__ draws)
+                                           const wcpt_draw_command* __restrict__ draws,
+                                           const uint64_t* __restrict__ tri_records)
 {
     Hit h;
     h.t = t;
@@ -417,12 +440,7 @@ __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t pri
             h.normal = (ph - c) / s.radius;                        /* :145 */
             h.material = s.material;
         } else {
-            const gu32_ptr idx = as_u32(draws[draw].indexBuffer);
-            const gf32_ptr vtx = as_f32(draws[draw].vertexBuffer);
-            const f3 a = ld3(vtx + 3ull * idx[prim + 0]);
-            const f3 b = ld3(vtx + 3ull * idx[prim + 1]);
-            const f3 c = ld3(vtx + 3ull * idx[prim + 2]);
-            h.normal = normalize(cross(b - a, c - a));                /* :173, material 0 (:175) */
+            h.normal = triangle_normal(prim, draw, draws, tri_records); /* :173, material 0 (:175) */
         }
         h.front = dot(ray.direction, h.normal) < 0.0f;
         if (!h.front) h.normal = h.normal * -1.0f;
@@ -570,7 +588,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     }
 
     if (COUNT && prim != kNoPrim) cnt.hits++;
-    return resolve_hit(ray, rt, prim, primDraw, spheres, draws);
+    return resolve_hit(ray, rt, prim, primDraw, spheres, draws, tri_records);
 }
 
 /* pathTracer.comp:213-234 */

@@ -138,7 +138,8 @@ __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restr
         for (int c2 = 0; c2 < 9; c2++) v[h][c2] = f[c2];
         singles[3ull * k + 0] = make_float4(a.x, a.y, a.z, e1.x);
         singles[3ull * k + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
-        singles[3ull * k + 2] = make_float4(e2.z, 0.0f, 0.0f, 0.0f);
+        const f3 n = normalize(cross(e1, e2)); /* :173 */
+        singles[3ull * k + 2] = make_float4(e2.z, n.x, n.y, n.z);
     }
     float4* o = out + (uint64_t)kPairRecordFloat4s * j;
     o[0] = make_float4(v[0][0], v[1][0], v[0][1], v[1][1]);

@@ -390,7 +390,9 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
 template <bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                         const wcpt_sphere* __restrict__ spheres,
-                                                        const wcpt_draw_command* __restrict__ draws, WfBuffers b, float4* __restrict__ image, uint32_t W,
+                                                        const wcpt_draw_command* __restrict__ draws,
+                                                        const uint64_t* __restrict__ tri_records, WfBuffers b,
+                                                        float4* __restrict__ image, uint32_t W,
                                                         uint32_t H, uint32_t y0, unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_wave[kShadeBlock / 64], s_base;
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
             sample = __float_as_uint(r1.w);
             seed = __float_as_uint(li.w);
             const uint32_t prim = __float_as_uint(hi.y);
-            const Hit h = resolve_hit(ps.ray, hi.x, prim, __float_as_uint(hi.z), spheres, draws);
+            const Hit h = resolve_hit(ps.ray, hi.x, prim, __float_as_uint(hi.z), spheres, draws, tri_records);
             if (COUNT && h.hit) cnt.hits++;
             f3 L;
             if (!path_shade(ps, h, seed, sd, mats, L)) {
@@ -582,7 +584,7 @@ static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace
     hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
                        a.tri_records, b, a.status, a.counters, a.wf_refill);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
-                       a.spheres, a.draws, b, a.image, a.W, a.H, a.y0, a.counters);
+                       a.spheres, a.draws, a.tri_records, b, a.image, a.W, a.H, a.y0, a.counters);
 }
 
 template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
