@@ -193,8 +193,16 @@ __device__ __forceinline__ float raySphereNear(const Ray& r, f3 position, float 
     return -b - sqrtf(t);
 }
 
-/* pathTracer.comp:121-133; returns t or -1 */
-/* pathTracer.comp:121-133 with the two edges given: e1 = b - a, e2 = c - a (:122-123) */
+/* The acceptance test of :132 without its `u <= 1` term, which the other terms imply: with v >= 0, u + v >= u
+ * exactly, so the rounded sum RN(u + v) >= RN(u) = u (rounding is monotonic), and u + v <= 1 then gives u <= 1.
+ * A NaN u or v fails `u >= 0` / `v >= 0` either way, and u = +inf fails `u + v <= 1`. Same decision, one
+ * compare less per triangle. */
+__device__ __forceinline__ bool accept_tri(float t, float u, float v, float uv)
+{
+    return t > 0.0f && u >= 0.0f && v >= 0.0f && uv <= 1.0f;
+}
+
+/* pathTracer.comp:121-133 with the two edges given: e1 = b - a, e2 = c - a (:122-123); returns t or -1 */
 __device__ __forceinline__ float rayTriangleE(const Ray& r, f3 a, f3 edgeAB, f3 edgeAC)
 {
     const f3 oa = r.origin - a;
@@ -204,7 +212,7 @@ __device__ __forceinline__ float rayTriangleE(const Ray& r, f3 a, f3 edgeAB, f3 
     const float u = dot(oa, crossRDE2) * inv;
     const float v = dot(r.direction, crossROAE1 * inv);
     const float t = dot(edgeAC, crossROAE1) * inv;
-    return (t > 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f) ? t : -1.0f;
+    return accept_tri(t, u, v, u + v) ? t : -1.0f;
 }
 __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { return rayTriangleE(r, a, b - a, c - a); }
 
@@ -282,8 +290,8 @@ __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& 
     const v2f uv = u + v;
     PairHit h;
     h.t = t;
-    h.hit0 = t.x > 0.0f && u.x >= 0.0f && u.x <= 1.0f && v.x >= 0.0f && uv.x <= 1.0f;
-    h.hit1 = t.y > 0.0f && u.y >= 0.0f && u.y <= 1.0f && v.y >= 0.0f && uv.y <= 1.0f;
+    h.hit0 = accept_tri(t.x, u.x, v.x, uv.x);
+    h.hit1 = accept_tri(t.y, u.y, v.y, uv.y);
     return h;
 }
 __device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
@@ -322,6 +330,15 @@ __device__ __forceinline__ void simd_step(uint32_t& wave, uint32_t& lane_steps)
     const unsigned long long m = __ballot(1);
     lane_steps++;
     if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) wave++;
+}
+
+template <bool COUNT, bool DIAG>
+__device__ __forceinline__ void count_tri(Counters& cnt)
+{
+    if (COUNT) {
+        cnt.triangle_tests++;
+        simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
+    }
 }
 
 /* Traversal stacks; entries = (node index, box entry distance t0) of deferred far children.
@@ -482,6 +499,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         const uint32_t ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
         const bool packed = (tri_records[kTriTableWords * i + 3u] & kTriFlagPackedRefs) != 0u;
         if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
+        const float rt_before = rt; /* a hit in this draw lowers rt (strict <): then it owns prim */
 
         /* root: pushed untested, popped and tested (:155-162) */
         NodeV cur = load_node(bvh, 0);
@@ -495,31 +513,28 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 /* leaf (:164-178) */
                 const uint32_t k0 = leaf_record(curLeft, curCount, ntri);
                 if (PAIRS && k0 != kNoRecord) {
+                    /* triangles [k0, kend) in pair records (2j, 2j+1): a leaf that starts in the second slot of
+                     * a pair tests that pair for its first triangle, then whole pairs, then possibly the first
+                     * slot of a last pair -- no per-iteration slot checks; applied in index order, strict < */
                     const uint32_t kend = k0 + (curCount + 2u) / 3u;
-                    for (uint32_t k = k0 & ~1u; k < kend; k += 2) {
+                    uint32_t k = k0;
+                    if (k & 1u) {
                         const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
-                        if (k >= k0) {
-                            if (COUNT) {
-                                cnt.triangle_tests++;
-                                simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
-                            }
-                            if (ph.hit0 && ph.t.x < rt) {
-                                rt = ph.t.x;
-                                prim = 3u * k;
-                                primDraw = i;
-                            }
-                        }
-                        if (k + 1u < kend) {
-                            if (COUNT) {
-                                cnt.triangle_tests++;
-                                simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
-                            }
-                            if (ph.hit1 && ph.t.y < rt) {
-                                rt = ph.t.y;
-                                prim = 3u * (k + 1u);
-                                primDraw = i;
-                            }
-                        }
+                        count_tri<COUNT, DIAG>(cnt);
+                        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
+                        k++;
+                    }
+                    for (const uint32_t kfull = kend & ~1u; k < kfull; k += 2) {
+                        const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
+                        count_tri<COUNT, DIAG>(cnt);
+                        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
+                        count_tri<COUNT, DIAG>(cnt);
+                        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * (k + 1u); }
+                    }
+                    if (k < kend) {
+                        const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
+                        count_tri<COUNT, DIAG>(cnt);
+                        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
                     }
                 } else {
                     for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
@@ -534,7 +549,6 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                         if (t != -1.0f && t < rt) {
                             rt = t;
                             prim = first;
-                            primDraw = i;
                         }
                     }
                 }
@@ -585,6 +599,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
             }
             if (!found) break;
         }
+        if (rt != rt_before) primDraw = i;
     }
 
     if (COUNT && prim != kNoPrim) cnt.hits++;
