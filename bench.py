@@ -28,7 +28,7 @@ sys.path[:0] = [os.path.join(ROOT, "wc-path-tracer_amd")]
 import numpy as np  # noqa: E402
 import wcpt  # noqa: E402
 from wcpt import scene as wscene  # noqa: E402
-from wcpt.dist import row_block  # noqa: E402
+from wcpt.dist import assemble, row_block  # noqa: E402
 
 CONFIGS = {
     # name: (scene, width, height, spp, maxBounceCount, description)
@@ -98,6 +98,9 @@ def main():
     ap.add_argument("--bvh", default="midpoint", choices=["midpoint", "sah"],
                     help="BVH builder: the reference's midpoint split (default: the benchmarked workload) or the "
                          "optional binned SAH (a different tree, reported as a separate workload)")
+    ap.add_argument("--gather", default="rgb", choices=["rgb", "rgba"],
+                    help="N>1 wire format of the row blocks: rgb (default; alpha is always 1.0 and is restored on "
+                         "rank 0, bit-identical frame, 12 B/px) or the full rgba32f block (16 B/px)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: gather each frame on the render stream instead of overlapping it with the next render")
     ap.add_argument("--verify", action="store_true",
@@ -141,13 +144,15 @@ def main():
     shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
     ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
     host_staged = world > 1 and args.dist_backend == "gloo-host"
-    gather_like = shard.cpu() if host_staged else shard
-    # Overlap: frame k's row block is copied (on the render stream, 16 B/px, ~2 us) into one of two staging
+    rgb = world > 1 and args.gather == "rgb"
+    wire = shard[..., :3] if rgb else shard            # what one frame puts on the wire (a view of the shard)
+    gather_like = torch.empty(wire.shape, dtype=wire.dtype, device="cpu" if host_staged else "cuda")
+    # Overlap: frame k's row block is copied (on the render stream, 12 or 16 B/px, a few us) into one of two staging
     # buffers and gathered on a separate communication stream while frame k+1 renders. Every frame is still
     # rendered and gathered; the timed region ends with a device-wide synchronize that includes the last gather.
     overlap = world > 1 and not args.no_overlap
     comm = torch.cuda.Stream(device=device) if overlap else None
-    staging = [torch.empty_like(shard) for _ in range(2)] if overlap else None
+    staging = [torch.empty(wire.shape, dtype=wire.dtype, device="cuda") for _ in range(2)] if overlap else None
     nbuf = 2 if overlap else 1
     gathered = [[torch.empty_like(gather_like) for _ in range(world)] for _ in range(nbuf)] \
         if (world > 1 and rank == 0) else None
@@ -170,11 +175,11 @@ def main():
         last["buf"] = i
         out = gathered[i] if rank == 0 else None
         if not overlap:
-            dist.gather(shard.cpu() if host_staged else shard, out, dst=0)
+            dist.gather(wire.cpu() if host_staged else wire.contiguous(), out, dst=0)
             return
         if done_used[i]:
             stream.wait_event(done_ev[i])               # staging[i] is free again
-        staging[i].copy_(shard, non_blocking=True)       # on the render stream, after this frame's render
+        staging[i].copy_(wire, non_blocking=True)        # on the render stream, after this frame's render
         ready_ev[i].record(stream)
         with torch.cuda.stream(comm):
             comm.wait_event(ready_ev[i])
@@ -221,8 +226,7 @@ def main():
     verified = None
     if args.verify and rank == 0:
         if world > 1:
-            frame_img = torch.cat([g[:row_block(H, world, r)[1]].to("cpu")
-                                   for r, g in enumerate(gathered[last["buf"]])], 0)
+            frame_img = assemble([g.to("cpu") for g in gathered[last["buf"]]], H, world)
         else:
             frame_img = shard[:H].to("cpu")
         with wcpt.Context(device) as vctx:
@@ -275,6 +279,7 @@ def main():
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel], "bvh": args.bvh,
                        "parallelism": f"row-block x{world}" + ((" + RCCL gather" if args.dist_backend == "nccl"
                                                                else f" + {args.dist_backend} gather (rehearsal)")
+                                                              + f" of {args.gather} blocks"
                                                               + (" overlapped with the next frame" if overlap else "")
                                                               if world > 1 else "")},
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),

@@ -37,7 +37,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, out_path):
+def _worker(rank, world, port, W, H, out_path, rgb_only=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "wc-path-tracer_amd"), os.path.join(root, "oracle")]
@@ -51,19 +51,20 @@ def _worker(rank, world, port, W, H, out_path):
     img, _ = oracle.render_scene(s, W, H, max_bounce=4, frame=3, y0=y0, rows=rows)
     shard = torch.zeros((-(-H // world), W, 4), dtype=torch.float32)
     shard[:rows] = torch.from_numpy(img)
-    frame = gather_frame(shard, H, world, rank)
+    frame = gather_frame(shard, H, world, rank, rgb_only=rgb_only)
     if rank == 0:
         np.save(out_path, frame.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_reassembles_frame(tmp_path, world):
+@pytest.mark.parametrize("world,rgb_only", [(2, False), (3, False), (2, True), (3, True)])
+def test_gather_reassembles_frame(tmp_path, world, rgb_only):
+    """Both wire formats (RGBA, and RGB with alpha restored on the presenting rank) give the 1-rank frame."""
     import oracle
     from wcpt import scene as wscene
     W, H = 48, 37
     out = str(tmp_path / "frame.npy")
-    mp.spawn(_worker, args=(world, _free_port(), W, H, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, out, rgb_only), nprocs=world, join=True)
     full, _ = oracle.render_scene(wscene.generate("cornell"), W, H, max_bounce=4, frame=3)
     assert np.array_equal(np.load(out), full)

@@ -1,17 +1,18 @@
 // Exhaustive check: is (v_rcp_f32 + one FMA Newton step) the correctly rounded reciprocal for every binary32 x
-// in a given range? Compares against 1.0f / x (hipcc's IEEE division) over all 2^32 bit patterns.
+// in a given range (default [2^-126, 2^126); argument "normal": every finite normal)? Compares against 1.0f / x (hipcc's IEEE division) over all 2^32 bit patterns.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
 
-__global__ void check(unsigned long long* mism, unsigned long long* first, uint32_t hi_bits)
+__global__ void check(unsigned long long* mism, unsigned long long* first, uint32_t hi_bits, int all_normals)
 {
     const uint64_t base = ((uint64_t)hi_bits << 24);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < (1u << 24); k += gridDim.x * blockDim.x) {
         const uint32_t bits = (uint32_t)(base + k);
         const float x = __uint_as_float(bits);
         const float a = fabsf(x);
-        if (!(a >= 0x1p-126f && a < 0x1p126f)) continue; /* the fast path's guarded range */
+        /* the fast path's guarded range, or (all_normals) every finite normal number */
+        if (all_normals ? !(a >= 0x1p-126f && a <= 0x1.fffffep127f) : !(a >= 0x1p-126f && a < 0x1p126f)) continue;
         const float ref = 1.0f / x;
         const float y = __builtin_amdgcn_rcpf(x);
         const float e = __builtin_fmaf(-x, y, 1.0f);
@@ -23,8 +24,9 @@ __global__ void check(unsigned long long* mism, unsigned long long* first, uint3
     }
 }
 
-int main()
+int main(int argc, char** argv)
 {
+    const int all_normals = argc > 1 && argv[1][0] == 'n'; /* "normal": extend to [2^126, 2^128) */
     unsigned long long *m, *f;
     hipMalloc(&m, 8);
     hipMalloc(&f, 8);
@@ -33,7 +35,7 @@ int main()
         unsigned long long z = 0, ff = ~0ull;
         hipMemcpy(m, &z, 8, hipMemcpyHostToDevice);
         hipMemcpy(f, &ff, 8, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(check, dim3(4096), dim3(256), 0, 0, m, f, hb);
+        hipLaunchKernelGGL(check, dim3(4096), dim3(256), 0, 0, m, f, hb, all_normals);
         unsigned long long c = 0, fb = 0;
         hipMemcpy(&c, m, 8, hipMemcpyDeviceToHost);
         hipMemcpy(&fb, f, 8, hipMemcpyDeviceToHost);
