@@ -94,7 +94,9 @@ def main():
                     help="0 megakernel, 2 wavefront, -1 per-config default (DEFAULT_KERNEL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC HBM-traffic summary for roofline.traffic (default profiles/pmc_traffic_<config>.json, "
+                         "written by tools/pmc_summary.py)")
     ap.add_argument("--bvh", default="midpoint", choices=["midpoint", "sah"],
                     help="BVH builder: the reference's midpoint split (default: the benchmarked workload) or the "
                          "optional binned SAH (a different tree, reported as a separate workload)")
@@ -253,13 +255,16 @@ def main():
         avg_kernel_s = kernel_ms / max(1, launches) / 1e3
         bytes_per_launch = algorithmic_bytes(tot) / args.steps
         achieved = bytes_per_launch / avg_kernel_s / 1e9
+        # PMC HBM bytes of the same unit as `achieved`: per launch (megakernel) or per frame (wavefront: all of a
+        # frame's launches), measured in separate rocprofv3 --pmc passes (profiles/README.md)
         traffic = None
-        if os.path.exists(args.pmc_json):
+        pmc_json = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
+        if os.path.exists(pmc_json):
             try:
-                pm = json.load(open(args.pmc_json))
-                if pm.get("config") == args.config and pm.get("kernel") == args.kernel:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
+                pm = json.load(open(pmc_json))
+                if pm.get("config") == args.config and pm.get("kernel") == args.kernel and args.bvh == "midpoint":
+                    traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_frame"))
+            except (OSError, ValueError):
                 traffic = None
         out = {
             "metric": BASELINE_METRIC,

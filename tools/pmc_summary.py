@@ -30,19 +30,37 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--config", default=None)
     ap.add_argument("--kernel-id", type=int, default=0)
+    ap.add_argument("--frame-kernel", default=None,
+                    help="whole-frame mode (wavefront: several kernels per frame): --kernel is a comma list of "
+                         "kernel filters whose counters are SUMMED over all their dispatches and divided by the "
+                         "dispatch count of this kernel (one per frame, e.g. 'wf_init<false')")
     a = ap.parse_args()
     per = load(a.dir)
     out = {}
-    for name, ctrs in per.items():
-        if a.kernel not in name:
-            continue
-        for c, vals in ctrs.items():
-            out[c] = sum(vals) / len(vals)
+    if a.frame_kernel:
+        frames = sum(len(next(iter(c.values()))) for n, c in per.items() if a.frame_kernel in n)
+        if not frames:
+            raise SystemExit(f"no dispatches of {a.frame_kernel} in {a.dir}")
+        filters = a.kernel.split(",")
+        for name, ctrs in per.items():
+            if not any(f in name for f in filters):
+                continue
+            for c, vals in ctrs.items():
+                out[c] = out.get(c, 0.0) + sum(vals) / frames
+        if not out:
+            raise SystemExit(f"no dispatches of {a.kernel} in {a.dir}")
+    else:
+        for name, ctrs in per.items():
+            if a.kernel not in name:
+                continue
+            for c, vals in ctrs.items():
+                out[c] = sum(vals) / len(vals)
     if not out:
         raise SystemExit(f"no dispatches of {a.kernel} in {a.dir}")
     d = dict(out)
     if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
-        d["hbm_bytes_per_launch"] = int((2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024)
+        key = "hbm_bytes_per_frame" if a.frame_kernel else "hbm_bytes_per_launch"
+        d[key] = int((2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024)
     if "SQ_ACTIVE_INST_VALU" in out and "SQ_THREAD_CYCLES_VALU" in out and out["SQ_ACTIVE_INST_VALU"]:
         d["valu_lane_utilization"] = out["SQ_THREAD_CYCLES_VALU"] / (64.0 * out["SQ_ACTIVE_INST_VALU"])
     if "SQ_WAVE_CYCLES" in out and out["SQ_WAVE_CYCLES"]:
