@@ -78,6 +78,16 @@ extern "C" {
 /* Wavefront trace: a wave fetches new rays once this many of its 64 lanes are idle (1..64, default 12: fewer,
  * fuller fetch rounds; c3 9.0 -> 8.2 ms against 1). */
 #define WCPT_OPTION_WF_REFILL 8
+/* Megakernel schedule. 0: one wave per 8x8 tile. k > 0: persistent waves (at most the chip's resident waves and at
+ * most ceil(tiles / k)) that regenerate paths per lane: a lane whose pixel is done takes the next pixel of a global
+ * queue, so waves do not wait for their longest path and small row blocks do not end on a tail. Same results. */
+#define WCPT_OPTION_MK_REGEN 9
+/* Regenerating megakernel: a wave fetches new pixels once this many of its 64 lanes are idle (1..64). */
+#define WCPT_OPTION_MK_REFILL 10
+/* Megakernel tile order: 0 each XCD walks a contiguous band of 8x8 tiles; 1 scattered (tile b * m mod tiles), so the
+ * tiles resident on a CU at once come from all over the frame; 2 (default) scattered when the launch fits in about
+ * one round of resident waves (small row blocks: the tail is the most loaded CU), banded otherwise. Same results. */
+#define WCPT_OPTION_MK_TILE_ORDER 11
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 
@@ -223,6 +233,13 @@ uint64_t wcpt_image_device_ptr(wcpt_context* ctx);                 /* float4[row
  * instead of the context's own image. `bytes` must hold width*rows*16. device_ptr == 0 reverts to the
  * context-owned image. The caller keeps ownership. */
 int      wcpt_set_external_image(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes);
+/* Gather payload written by the render itself: every wcpt_render also stores each pixel it
+ * finishes into caller-owned device memory at `device_ptr` -- row-major float[rows][width][channels], channels 3
+ * (RGB; alpha is always 1.0, pathTracer.comp:323) or 4 (RGBA) -- the same values as the accumulation image. A
+ * multi-GPU host points it at the buffer it hands to the collective, so no copy kernel sits between the render and
+ * the gather. `bytes` must hold width*rows*channels*4 at render time. device_ptr == 0 turns it off. Takes effect
+ * for the next render; no synchronisation. The caller keeps ownership. */
+int      wcpt_set_gather_output(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes, uint32_t channels);
 int      wcpt_readback(wcpt_context* ctx, float* dst, uint64_t bytes);
 int      wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes); /* seed accumulation */
 

@@ -77,6 +77,7 @@ def test_no_device_errors_cleanly():
 def test_null_handles_rejected():
     assert wcpt.lib.wcpt_render(None, None, 0, 0, 0) == -1001
     assert wcpt.lib.wcpt_sync(None) == -1001
+    assert wcpt.lib.wcpt_set_gather_output(None, 0, 0, 3) == -1001
     assert wcpt.lib.wcpt_buffer_device_address(None, 1) == 0
     assert wcpt.lib.wcpt_destroy(None) == 0
     n = C.c_int(-1)

@@ -620,3 +620,106 @@ def test_random_scenes_match_oracle(gpu_ctx, seed, kernel):
     ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, image=init, threads=8)
     assert_close(img, ref)
     assert cnt == rcnt
+
+
+@pytest.mark.parametrize("regen,refill", [(1, 16), (1, 1), (1, 64), (3, 8), (1000, 16)])
+@pytest.mark.parametrize("name,W,H,bounces,spp,frame", [
+    ("cornell", 67, 45, 4, 3, 0),        # ragged, several samples per pixel
+    ("default_dielectric", 48, 40, 3, 1, 7),
+    ("atrium", 96, 54, 4, 1, 2),
+    ("cornell", 40, 24, 4, 0, 0),        # samples = 0: the reference's 0/0 pixels
+])
+def test_regen_megakernel_matches_oracle(gpu_ctx, regen, refill, name, W, H, bounces, spp, frame):
+    """The persistent megakernel with per-lane path regeneration (WCPT_OPTION_MK_REGEN) renders exactly the
+    oracle's image and counts exactly its work: only which lane runs which pixel, and when, changes."""
+    s = get_scene(name)
+    init = np.random.default_rng(5).uniform(0, 1, (H, W, 4)).astype(np.float32)
+    gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, regen)
+    gpu_ctx.set_option(wcpt._lib.OPTION_MK_REFILL, refill)
+    try:
+        img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, init=init)
+        # twice in a row: the second launch runs on the other pixel-queue head
+        img2, _ = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, init=init)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, 0)
+        gpu_ctx.set_option(wcpt._lib.OPTION_MK_REFILL, 16)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, image=init, threads=8)
+    if spp == 0:
+        assert np.isnan(ref[..., :3]).all() and np.isnan(img[..., :3]).all() and np.isnan(img2[..., :3]).all()
+        assert np.array_equal(img[..., 3], ref[..., 3])
+    else:
+        assert_close(img, ref)
+        assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
+    assert cnt == rcnt
+
+
+def test_regen_megakernel_row_blocks(gpu_ctx):
+    """Row blocks of the regenerating megakernel equal the full frame (and the static schedule's frame)."""
+    s = get_scene("cornell")
+    W, H = 1920, 1080
+    full, _ = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=3, init=np.zeros((H, W, 4), np.float32))
+    gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, 2)
+    try:
+        for n in (8, 3):
+            parts = []
+            for r in range(n):
+                y0, rows = row_block(H, n, r)
+                img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=3, y0=y0, rows=rows,
+                                      init=np.zeros((rows, W, 4), np.float32))
+                assert cnt["pixels"] == rows * W
+                parts.append(img)
+            assert np.array_equal(np.concatenate(parts).view(np.uint32), full.view(np.uint32))
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, 0)
+
+
+@pytest.mark.parametrize("name,W,H,bounces,spp,rows", [
+    ("cornell", 67, 45, 4, 3, None), ("atrium", 96, 54, 4, 1, None), ("cornell", 1920, 1080, 4, 1, 135)])
+def test_scattered_tile_order_matches_oracle(gpu_ctx, name, W, H, bounces, spp, rows):
+    """WCPT_OPTION_MK_TILE_ORDER = 1 (scattered tiles) changes only which wave renders which tile."""
+    s = get_scene(name)
+    gpu_ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, 1)
+    try:
+        img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=1, rows=rows,
+                              init=np.zeros((rows or H, W, 4), np.float32))
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, 2)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=1, rows=rows, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("channels", [3, 4])
+def test_gather_output_equals_image(gpu_ctx, kernel, channels):
+    """wcpt_set_gather_output: the render writes each pixel of its row block into the payload buffer too (RGB or
+    RGBA), bit-identical to the accumulation image, including progressive frames and a row block."""
+    s = get_scene("cornell")
+    W, H = 96, 80
+    y0, rows = row_block(H, 3, 1)
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    gpu_ctx.set_kernel(kernel)
+    nbytes = rows * W * channels * 4
+    buf = gpu_ctx.buffer_from(np.full(rows * W * channels, -7.0, np.float32))
+    try:
+        gpu_ctx.create_screen(W, H)
+        gpu_ctx.set_row_range(y0, rows)
+        init = np.random.default_rng(2).uniform(0, 1, (rows, W, 4)).astype(np.float32)
+        gpu_ctx.image_upload(init)
+        for frame in (0, 1, 2):
+            gpu_ctx.set_gather_output(gpu_ctx.buffer_address(buf), nbytes, channels)
+            gpu_ctx.render(s.scene_data(W, H, max_bounce=4, frame=frame), *dev.addresses())
+            gpu_ctx.sync()
+            img = gpu_ctx.readback(rows)
+            got = np.frombuffer(gpu_ctx.buffer_download(buf, nbytes), np.float32).reshape(rows, W, channels)
+            assert np.array_equal(got.view(np.uint32), img[..., :channels].view(np.uint32))
+        # too small for the row block -> error, no launch
+        gpu_ctx.set_gather_output(gpu_ctx.buffer_address(buf), nbytes - 4, channels)
+        with pytest.raises(wcpt.WcptError):
+            gpu_ctx.render(s.scene_data(W, H, max_bounce=4, frame=3), *dev.addresses())
+    finally:
+        gpu_ctx.set_gather_output(0, 0)
+        gpu_ctx.set_row_range(0, 0)
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        gpu_ctx.buffer_free(buf)
+        dev.free()

@@ -2,12 +2,15 @@
 
     python tools/ab.py --config c3 --variants "kernel=0" "kernel=2" "kernel=2,deindex=1" [--frames 5 --rounds 3]
 
-Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, deindex=<0|1> (mesh re-laid out in
+Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, regen=<k>, mkrefill=<1..64>, deindex=<0|1> (mesh re-laid out in
 BVH leaf order with identity indices: same triangles, same results, soup-like locality). Prints the median
 ms/frame (HIP events on the context stream) and Mray/s.
 """
 import argparse
 import os
+
+if os.environ.get("AB_TORCH_FIRST"):  # bench.py's load order: libwcpt then binds to torch's HIP runtime
+    import torch  # noqa: F401
 import statistics
 import sys
 
@@ -40,6 +43,7 @@ def main():
     ap.add_argument("--variants", nargs="+", default=["kernel=0"])
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=0, help="render rows [0, rows) only (a row block of an N-way split)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
@@ -48,6 +52,8 @@ def main():
     if any(parse(v).get("deindex") == "1" for v in a.variants):
         scenes["1"] = wcpt.DeviceScene(ctx, deindexed(s))
     ctx.create_screen(W, H)
+    if a.rows:
+        ctx.set_row_range(0, a.rows)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
     segs = sum(ctx.render_counters(sd, *scenes["0"].addresses())["segments"] for sd in sds)
     res = {v: [] for v in a.variants}
@@ -61,6 +67,9 @@ def main():
             ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, int(o.get("pairs", -1)))
             ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, int(o.get("refs", 1)))
             ctx.set_option(wcpt._lib.OPTION_WF_REFILL, int(o.get("refill", 12)))
+            ctx.set_option(wcpt._lib.OPTION_MK_REGEN, int(o.get("regen", 0)))
+            ctx.set_option(wcpt._lib.OPTION_MK_REFILL, int(o.get("mkrefill", 16)))
+            ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, int(o.get("order", 2)))
             dev = scenes[o.get("deindex", "0")]
             ctx.profile_begin()
             for sd in sds:

@@ -739,6 +739,24 @@ __device__ __forceinline__ f3 primary_direction(const wcpt_scene_data& sd, uint3
     return normalize(mk3(wd[0], wd[1], wd[2]));
 }
 
+/* Final store of a pixel (pathTracer.comp:323, `vec4(acc, 1)`): the accumulation image, plus the gather payload
+ * (wcpt_set_gather_output) when the host asked for one -- RGB (3 floats) or RGBA, same row-major pixel index. */
+__device__ __forceinline__ void store_pixel(float4* __restrict__ image, float* __restrict__ wire, uint32_t wire_ch,
+                                            size_t i, f3 acc)
+{
+    image[i] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+    if (wire) {
+        if (wire_ch == 3u) {
+            float* w = wire + 3u * i;
+            w[0] = acc.x;
+            w[1] = acc.y;
+            w[2] = acc.z;
+        } else {
+            reinterpret_cast<float4*>(wire)[i] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        }
+    }
+}
+
 /* Wave-level sum of a per-lane u32 counter, one u64 atomic per wave. */
 __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v)
 {

@@ -25,7 +25,13 @@ struct LaunchArgs {
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
+    uint32_t mk_regen;           /* megakernel: 0 one tile per wave; k > 0 persistent waves with per-lane path
+                                    regeneration, at most ceil(tiles / k) waves (WCPT_OPTION_MK_REGEN) */
+    uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto (WCPT_OPTION_MK_TILE_ORDER) */
+    uint32_t mk_refill;          /* regenerating megakernel: idle lanes that trigger a pixel fetch (1..64) */
     float4* image;
+    float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
+    uint32_t wire_ch;            /* its channels per pixel: 3 or 4 */
     uint32_t W, H, y0, rows;
     uint32_t* status;
     unsigned long long* counters;
@@ -53,6 +59,8 @@ struct WfBuffers {
     uint32_t* count_out;
     uint32_t* head;    /* trace kernel's dequeue position                               */
     unsigned long long* diag; /* DIAG builds: trace-loop phase timers (8 x u64)         */
+    float* wire;       /* gather payload (LaunchArgs::wire) or null                     */
+    uint32_t wire_ch;
 };
 struct WfState {
     void* mem = nullptr;
@@ -69,6 +77,15 @@ struct WfState {
     int trace_bpc[3][2][3] = {};   /* trace-kernel blocks per CU by (mode, single draw, LDS stack variant)  */
 };
 
+/* Regenerating megakernel schedule: per-context state. Each launch dequeues pixels from head[parity] and zeroes
+ * head[parity ^ 1] for the next launch on the stream (launches on one stream never overlap). */
+struct MkState {
+    uint32_t* head = nullptr;  /* 2 x u32, zero-initialised */
+    uint32_t parity = 0;
+    int cus = 0;
+    int bpc[2][2][2] = {};     /* resident blocks per CU by (count build, stack kind, pair records) */
+};
+
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD
  * diagnostics (ballot-based step counters, tools/diag.py). */
 constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
@@ -80,7 +97,7 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
                                     void* pairs, hipStream_t stream);
 /* composite.comp (pt_composite.hip): gamma + PBR Neutral over `pixels` float4 texels into rgba32f or RGBA8 */
 hipError_t launch_composite(const float4* img, uint64_t pixels, void* dst, bool rgba8, int cus, hipStream_t stream);
-hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, hipStream_t stream);
+hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream);
 /* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
 /* lds_stack: LDS traversal-stack entries per lane of the trace kernel (10, 16 or 24; render mode only). */
 hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, int lds_stack,

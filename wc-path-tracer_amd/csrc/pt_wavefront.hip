@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
                     live = true;
                 } else { /* samples == 0: result / 0 = NaN (:312), stored as the reference would */
                     const f3 r = mk3(0.0f, 0.0f, 0.0f) / (float)sd.samples;
-                    if (!COUNT) image[(size_t)ly * W + lx] = make_float4(r.x, r.y, r.z, 1.0f);
+                    if (!COUNT) store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, r);
                     if (COUNT) cnt.pixels++;
                 }
             }
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
                             acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight,
                                       o.z * iw + result.z * weight);
                         }
-                        *px = make_float4(acc.x, acc.y, acc.z, 1.0f);
+                        store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, acc); /* :323 */
                     }
                     if (COUNT) cnt.pixels++;
                 }
@@ -678,6 +678,8 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
         e = hipMemsetAsync(s.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
     }
+    b.wire = a.wire;
+    b.wire_ch = a.wire_ch;
     b.count_in = s.ctr + 0;
     b.count_out = s.ctr + 1;
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);

@@ -86,11 +86,15 @@ struct wcpt_context {
     float4* own_image = nullptr;
     uint64_t image_bytes_cap = 0;
     uint64_t external_bytes = 0;       /* != 0 while an external image is attached */
+    float* wire = nullptr;             /* wcpt_set_gather_output */
+    uint64_t wire_bytes = 0;
+    uint32_t wire_ch = 3;
     uint32_t width = 0, height = 0, y0 = 0, rows = 0; /* rows == height when not sharded */
     bool sharded = false;
     uint32_t* d_status = nullptr;
     unsigned long long* d_counters = nullptr;
     wcpt::WfState wf;                  /* path state of the wavefront kernels (allocated on first use) */
+    wcpt::MkState mk;                  /* pixel queue heads of the regenerating megakernel */
     uint32_t* d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
@@ -102,6 +106,9 @@ struct wcpt_context {
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (measured optimum 8..16 on c3) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
+    int mk_regen = 0;                  /* WCPT_OPTION_MK_REGEN */
+    int mk_refill = 16;                /* WCPT_OPTION_MK_REFILL */
+    int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
     std::vector<TriRecords> tri;       /* per draw command index */
     std::vector<uint64_t> tri_table;   /* host image of d_tri_table: {address, ntri} per draw */
@@ -317,6 +324,14 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.spheres = reinterpret_cast<const wcpt_sphere*>(spheres);
     a.draws = reinterpret_cast<const wcpt_draw_command*>(draws);
     a.image = ctx->image;
+    a.wire = nullptr;
+    a.wire_ch = ctx->wire_ch;
+    if (ctx->wire && mode == wcpt::kModeRender) {
+        if ((uint64_t)ctx->width * ctx->rows * ctx->wire_ch * 4ull > ctx->wire_bytes)
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%u x %u",
+                             (unsigned long long)ctx->wire_bytes, ctx->width, ctx->rows, ctx->wire_ch);
+        a.wire = ctx->wire;
+    }
     a.W = ctx->width;
     a.H = ctx->height;
     a.y0 = ctx->y0;
@@ -326,12 +341,16 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.tri_records = nullptr;
     a.pair_records = false;
     a.wf_refill = (uint32_t)ctx->wf_refill;
+    a.mk_regen = (uint32_t)ctx->mk_regen;
+    a.mk_refill = (uint32_t)ctx->mk_refill;
+    a.mk_tile_order = (uint32_t)ctx->mk_tile_order;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ctx->profiling && mode == wcpt::kModeRender) {
         if (ctx->events_used == ctx->events.size()) {
             hipEvent_t b, c;
-            HIP_TRY(ctx, hipEventCreate(&b), "hipEventCreate");
-            HIP_TRY(ctx, hipEventCreate(&c), "hipEventCreate");
+            /* device-scope release: timing only, no system-scope cache writeback between the timed launches */
+            HIP_TRY(ctx, hipEventCreateWithFlags(&b, hipEventReleaseToDevice), "hipEventCreate");
+            HIP_TRY(ctx, hipEventCreateWithFlags(&c, hipEventReleaseToDevice), "hipEventCreate");
             ctx->events.emplace_back(b, c);
         }
         e0 = ctx->events[ctx->events_used].first;
@@ -343,7 +362,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     if (rc) return rc;
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
-    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->stream); break;
+    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->mk, ctx->stream); break;
     case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream); break;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
     }
@@ -413,6 +432,8 @@ int wcpt_create(int device, wcpt_context** out_ctx)
     if (e == hipSuccess) e = hipMalloc(&ctx->d_status, 4);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_counters, kNumCounters * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 4);
+    if (e == hipSuccess) e = hipMalloc(&ctx->mk.head, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(ctx->mk.head, 0, 2 * sizeof(uint32_t));
     if (e != hipSuccess) {
         int rc = hip_fail(nullptr, e, "wcpt_create");
         wcpt_destroy(ctx);
@@ -433,6 +454,7 @@ int wcpt_destroy(wcpt_context* ctx)
     if (ctx->own_image) (void)hipFree(ctx->own_image);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->mk.head) (void)hipFree(ctx->mk.head);
     wcpt::wf_release(ctx->wf);
     for (auto& t : ctx->tri)
         if (t.mem) (void)hipFree(t.mem);
@@ -475,6 +497,18 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     case WCPT_OPTION_WF_REFILL:
         if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
         ctx->wf_refill = value;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_MK_REGEN:
+        if (value < 0 || value > 1024) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "megakernel regeneration %d", value);
+        ctx->mk_regen = value;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_MK_REFILL:
+        if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
+        ctx->mk_refill = value;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_MK_TILE_ORDER:
+        if (value < 0 || value > 2) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "tile order %d", value);
+        ctx->mk_tile_order = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PACKED_REFS:
         ctx->packed_refs = value ? 1 : 0;
@@ -670,6 +704,27 @@ int wcpt_set_external_image(wcpt_context* ctx, uint64_t device_ptr, uint64_t byt
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "external image too small for %ux%u", ctx->width, ctx->rows);
     ctx->external_bytes = bytes;
     ctx->image = reinterpret_cast<float4*>(device_ptr);
+    return WCPT_SUCCESS;
+}
+
+int wcpt_set_gather_output(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes, uint32_t channels)
+{
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    if (device_ptr == 0) {
+        ctx->wire = nullptr;
+        ctx->wire_bytes = 0;
+        return WCPT_SUCCESS;
+    }
+    if (channels != 3 && channels != 4)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output channels %u (3 or 4)", channels);
+    if (bytes == 0 || (device_ptr & 3u))
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output: %llu bytes at a misaligned or empty buffer",
+                         (unsigned long long)bytes);
+    if (channels == 4 && (device_ptr & 15u))
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output: RGBA needs 16-byte alignment");
+    ctx->wire = reinterpret_cast<float*>(device_ptr);
+    ctx->wire_bytes = bytes;
+    ctx->wire_ch = channels;
     return WCPT_SUCCESS;
 }
 

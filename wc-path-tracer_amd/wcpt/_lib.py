@@ -48,6 +48,9 @@ OPTION_TRIANGLE_CACHE = 5
 OPTION_PAIR_RECORDS = 6
 OPTION_PACKED_REFS = 7
 OPTION_WF_REFILL = 8
+OPTION_MK_REGEN = 9
+OPTION_MK_REFILL = 10
+OPTION_MK_TILE_ORDER = 11
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
@@ -122,6 +125,7 @@ _PROTOTYPES = {
     "wcpt_set_row_range": (_i, [_p, _u32, _u32]),
     "wcpt_image_device_ptr": (_u64, [_p]),
     "wcpt_set_external_image": (_i, [_p, _u64, _u64]),
+    "wcpt_set_gather_output": (_i, [_p, _u64, _u64, _u32]),
     "wcpt_readback": (_i, [_p, _p, _u64]),
     "wcpt_image_upload": (_i, [_p, _p, _u64]),
     "wcpt_composite": (_i, [_p, _u64, _i]),

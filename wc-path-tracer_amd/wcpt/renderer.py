@@ -107,6 +107,10 @@ class Context:
     def set_external_image(self, device_ptr: int, nbytes: int):
         self._chk(lib.wcpt_set_external_image(self.h, device_ptr, nbytes))
 
+    def set_gather_output(self, device_ptr: int, nbytes: int, channels: int = 3):
+        """The render also writes each pixel into float[rows][width][channels] at device_ptr (0 = off)."""
+        self._chk(lib.wcpt_set_gather_output(self.h, device_ptr, nbytes, channels))
+
     def image_ptr(self) -> int:
         return lib.wcpt_image_device_ptr(self.h)
 
