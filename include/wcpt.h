@@ -59,7 +59,7 @@ extern "C" {
 #define WCPT_KERNEL_WAVEFRONT   2  /* split ray-gen / traverse / shade queues (same semantics)         */
 
 /* ---- tuning options (wcpt_set_option); none changes results ------------------------------------- */
-#define WCPT_OPTION_STACK       1  /* megakernel traversal stack: 0 = scratch (default), 1 = LDS + spill */
+#define WCPT_OPTION_STACK       1  /* megakernel traversal stack: 0 = scratch, 1 = LDS + spill (default) */
 #define WCPT_OPTION_DIAGNOSTICS 2  /* 1: wcpt_render_counters also fills the SIMD-efficiency fields      */
 #define WCPT_OPTION_SORT_RAYS   3  /* wavefront: sort bounce rays by (octant, origin Morton) (default 0) */
 #define WCPT_OPTION_WF_STACK    4  /* wavefront: LDS traversal-stack entries per lane, 10 | 16 | 24 (default 10) */
@@ -78,16 +78,10 @@ extern "C" {
 /* Wavefront trace: a wave fetches new rays once this many of its 64 lanes are idle (1..64, default 12: fewer,
  * fuller fetch rounds; c3 9.0 -> 8.2 ms against 1). */
 #define WCPT_OPTION_WF_REFILL 8
-/* Megakernel schedule. 0: one wave per 8x8 tile. k > 0: persistent waves (at most the chip's resident waves and at
- * most ceil(tiles / k)) that regenerate paths per lane: a lane whose pixel is done takes the next pixel of a global
- * queue, so waves do not wait for their longest path and small row blocks do not end on a tail. Same results. */
-#define WCPT_OPTION_MK_REGEN 9
-/* Regenerating megakernel: a wave fetches new pixels once this many of its 64 lanes are idle (1..64). */
-#define WCPT_OPTION_MK_REFILL 10
 /* Megakernel tile order: 0 each XCD walks a contiguous band of 8x8 tiles; 1 scattered (tile b * m mod tiles), so the
  * tiles resident on a CU at once come from all over the frame; 2 (default) scattered when the launch fits in about
  * one round of resident waves (small row blocks: the tail is the most loaded CU), banded otherwise. Same results. */
-#define WCPT_OPTION_MK_TILE_ORDER 11
+#define WCPT_OPTION_MK_TILE_ORDER 9
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

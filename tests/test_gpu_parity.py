@@ -622,57 +622,6 @@ def test_random_scenes_match_oracle(gpu_ctx, seed, kernel):
     assert cnt == rcnt
 
 
-@pytest.mark.parametrize("regen,refill", [(1, 16), (1, 1), (1, 64), (3, 8), (1000, 16)])
-@pytest.mark.parametrize("name,W,H,bounces,spp,frame", [
-    ("cornell", 67, 45, 4, 3, 0),        # ragged, several samples per pixel
-    ("default_dielectric", 48, 40, 3, 1, 7),
-    ("atrium", 96, 54, 4, 1, 2),
-    ("cornell", 40, 24, 4, 0, 0),        # samples = 0: the reference's 0/0 pixels
-])
-def test_regen_megakernel_matches_oracle(gpu_ctx, regen, refill, name, W, H, bounces, spp, frame):
-    """The persistent megakernel with per-lane path regeneration (WCPT_OPTION_MK_REGEN) renders exactly the
-    oracle's image and counts exactly its work: only which lane runs which pixel, and when, changes."""
-    s = get_scene(name)
-    init = np.random.default_rng(5).uniform(0, 1, (H, W, 4)).astype(np.float32)
-    gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, regen)
-    gpu_ctx.set_option(wcpt._lib.OPTION_MK_REFILL, refill)
-    try:
-        img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, init=init)
-        # twice in a row: the second launch runs on the other pixel-queue head
-        img2, _ = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, init=init)
-    finally:
-        gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, 0)
-        gpu_ctx.set_option(wcpt._lib.OPTION_MK_REFILL, 16)
-    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, image=init, threads=8)
-    if spp == 0:
-        assert np.isnan(ref[..., :3]).all() and np.isnan(img[..., :3]).all() and np.isnan(img2[..., :3]).all()
-        assert np.array_equal(img[..., 3], ref[..., 3])
-    else:
-        assert_close(img, ref)
-        assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
-    assert cnt == rcnt
-
-
-def test_regen_megakernel_row_blocks(gpu_ctx):
-    """Row blocks of the regenerating megakernel equal the full frame (and the static schedule's frame)."""
-    s = get_scene("cornell")
-    W, H = 1920, 1080
-    full, _ = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=3, init=np.zeros((H, W, 4), np.float32))
-    gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, 2)
-    try:
-        for n in (8, 3):
-            parts = []
-            for r in range(n):
-                y0, rows = row_block(H, n, r)
-                img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=3, y0=y0, rows=rows,
-                                      init=np.zeros((rows, W, 4), np.float32))
-                assert cnt["pixels"] == rows * W
-                parts.append(img)
-            assert np.array_equal(np.concatenate(parts).view(np.uint32), full.view(np.uint32))
-    finally:
-        gpu_ctx.set_option(wcpt._lib.OPTION_MK_REGEN, 0)
-
-
 @pytest.mark.parametrize("name,W,H,bounces,spp,rows", [
     ("cornell", 67, 45, 4, 3, None), ("atrium", 96, 54, 4, 1, None), ("cornell", 1920, 1080, 4, 1, 135)])
 def test_scattered_tile_order_matches_oracle(gpu_ctx, name, W, H, bounces, spp, rows):

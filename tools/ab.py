@@ -2,7 +2,7 @@
 
     python tools/ab.py --config c3 --variants "kernel=0" "kernel=2" "kernel=2,deindex=1" [--frames 5 --rounds 3]
 
-Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, regen=<k>, mkrefill=<1..64>, deindex=<0|1> (mesh re-laid out in
+Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, order=<0|1|2>, deindex=<0|1> (mesh re-laid out in
 BVH leaf order with identity indices: same triangles, same results, soup-like locality). Prints the median
 ms/frame (HIP events on the context stream) and Mray/s.
 """
@@ -60,15 +60,13 @@ def main():
     for r in range(a.rounds + 1):
         for v in a.variants:
             o = parse(v)
-            ctx.set_option(wcpt._lib.OPTION_STACK, int(o.get("stack", 0)))
+            ctx.set_option(wcpt._lib.OPTION_STACK, int(o.get("stack", 1)))
             ctx.set_kernel(int(o.get("kernel", 0)))
             ctx.set_option(wcpt._lib.OPTION_SORT_RAYS, int(o.get("sort", 0)))
             ctx.set_option(wcpt._lib.OPTION_WF_STACK, int(o.get("lds", 10)))
             ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, int(o.get("pairs", -1)))
             ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, int(o.get("refs", 1)))
             ctx.set_option(wcpt._lib.OPTION_WF_REFILL, int(o.get("refill", 12)))
-            ctx.set_option(wcpt._lib.OPTION_MK_REGEN, int(o.get("regen", 0)))
-            ctx.set_option(wcpt._lib.OPTION_MK_REFILL, int(o.get("mkrefill", 16)))
             ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, int(o.get("order", 2)))
             dev = scenes[o.get("deindex", "0")]
             ctx.profile_begin()

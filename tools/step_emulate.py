@@ -31,8 +31,6 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--regen", type=int, default=None, help="WCPT_OPTION_MK_REGEN (default: the library's)")
-    ap.add_argument("--mkrefill", type=int, default=None, help="WCPT_OPTION_MK_REFILL")
     ap.add_argument("--order", type=int, default=None, help="WCPT_OPTION_MK_TILE_ORDER")
     ap.add_argument("--ns", default="1,2,4,8", help="row-block splits to emulate")
     ap.add_argument("--variant", default="gather", choices=["gather", "events", "copy", "inline", "streamwait", "nowait"],
@@ -54,10 +52,6 @@ def main():
     ctx = wcpt.Context(0)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_kernel(DEFAULT_KERNEL[args.config])
-    if args.regen is not None:
-        ctx.set_option(wcpt._lib.OPTION_MK_REGEN, args.regen)
-    if args.mkrefill is not None:
-        ctx.set_option(wcpt._lib.OPTION_MK_REFILL, args.mkrefill)
     if args.order is not None:
         ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, args.order)
     dev = wcpt.DeviceScene(ctx, scene)

@@ -25,10 +25,7 @@ struct LaunchArgs {
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
-    uint32_t mk_regen;           /* megakernel: 0 one tile per wave; k > 0 persistent waves with per-lane path
-                                    regeneration, at most ceil(tiles / k) waves (WCPT_OPTION_MK_REGEN) */
     uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto (WCPT_OPTION_MK_TILE_ORDER) */
-    uint32_t mk_refill;          /* regenerating megakernel: idle lanes that trigger a pixel fetch (1..64) */
     float4* image;
     float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
     uint32_t wire_ch;            /* its channels per pixel: 3 or 4 */
@@ -77,13 +74,9 @@ struct WfState {
     int trace_bpc[3][2][3] = {};   /* trace-kernel blocks per CU by (mode, single draw, LDS stack variant)  */
 };
 
-/* Regenerating megakernel schedule: per-context state. Each launch dequeues pixels from head[parity] and zeroes
- * head[parity ^ 1] for the next launch on the stream (launches on one stream never overlap). */
+/* Megakernel launch state, per context. */
 struct MkState {
-    uint32_t* head = nullptr;  /* 2 x u32, zero-initialised */
-    uint32_t parity = 0;
-    int cus = 0;
-    int bpc[2][2][2] = {};     /* resident blocks per CU by (count build, stack kind, pair records) */
+    int cus = 0;               /* CU count of the context's device (0 = not yet queried) */
 };
 
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD

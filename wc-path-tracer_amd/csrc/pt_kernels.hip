@@ -10,8 +10,6 @@
  * __ballot inside the traversal loop (tools/diag.py only — kept out of the COUNT build the parity tests use).
  */
 #include <hip/hip_runtime.h>
-#include <stdio.h>
-#include <stdlib.h>
 
 #include "pt_device.h"
 #include "pt_kernels.h"
@@ -125,124 +123,6 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
     flush_counters<COUNT>(cnt, counters);
 }
 
-/* Persistent megakernel with per-lane path regeneration (WCPT_OPTION_MK_REGEN; Novak et al., "GPU computing:
- * dynamic path regeneration"). A resident wave loops over segments (one Intersect + shade per active lane per
- * iteration); a lane whose pixel is finished idles until at least `refill` lanes of its wave are idle, and then the
- * idle lanes take the next pixels of a global queue together (one atomicAdd per wave). Pixels are dequeued in
- * 8x8-tile order, so a full refill is one coherent tile. Every pixel is still computed by exactly the per-pixel
- * program of pathTracer.comp:290-323 (same seed, same RNG sequence, same sample loop), so the image and the work
- * counters equal the one-tile-per-wave kernel's; only which lane runs which pixel, and when, changes. What it
- * removes: the idle tail of a wave whose lanes finish at different bounces (a tile waits for its longest path),
- * and the tail of a launch whose tiles do not fill the chip evenly (small row blocks, N > 1). */
-template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
-__device__ __forceinline__ void regen_loop(const wcpt_scene_data& sd, const wcpt_material* __restrict__ mats,
-                                           const wcpt_sphere* __restrict__ spheres,
-                                           const wcpt_draw_command* __restrict__ draws,
-                                           const uint64_t* __restrict__ tri_records, float4* __restrict__ image,
-                                           float* __restrict__ wire, uint32_t wire_ch,
-                                           uint32_t W, uint32_t H, uint32_t y0, uint32_t rows, uint32_t tilesX,
-                                           uint32_t total, uint32_t* __restrict__ head, uint32_t refill, Stack& stk,
-                                           Counters& cnt, bool& overflow)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const f3 origin = mk3(sd.position[0], sd.position[1], sd.position[2]);
-    PathState ps;
-    uint32_t rng = 0, s = 0, lx = 0, ly = 0;
-    f3 result = mk3(0.0f, 0.0f, 0.0f);
-    bool active = false;
-    bool exhausted = false; /* wave-uniform: the queue has no pixels left */
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (nidle == 64u && exhausted) break;
-        if (!exhausted && (nidle >= refill || nidle == 64u)) {
-            uint32_t base = 0;
-            if (lane == (uint32_t)(__ffsll((long long)idle) - 1)) base = atomicAdd(head, nidle);
-            base = __shfl(base, __ffsll((long long)idle) - 1, 64);
-            if (base >= total || total - base <= nidle) exhausted = true;
-            if (!active) {
-                const uint32_t p = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (p < total) {
-                    const uint32_t tile = p >> 6, l = p & 63u;
-                    lx = (tile % tilesX) * kTileW + (l % kTileW);
-                    ly = (tile / tilesX) * kTileH + (l / kTileW);
-                    if (lx < W && ly < rows) {
-                        const uint32_t y = y0 + ly;
-                        rng = pcg_hash(lx + y * W + sd.renderedFramesCount * 719393u); /* :304-305 */
-                        result = mk3(0.0f, 0.0f, 0.0f);
-                        s = 0;
-                        active = true;
-                        if (sd.samples > 0) path_begin(ps, origin, primary_direction(sd, lx, y, W, H));
-                    }
-                }
-            }
-        }
-        if (active && s < sd.samples) {
-            const Hit h = intersect<COUNT, DIAG, PAIRS>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
-            f3 L;
-            if (path_shade(ps, h, rng, sd, mats, L)) {
-                result = result + L; /* :310 */
-                s++;
-                if (s < sd.samples) path_begin(ps, origin, primary_direction(sd, lx, y0 + ly, W, H));
-            }
-        }
-        if (active && s >= sd.samples) {
-            result = result / (float)sd.samples; /* :312 */
-            if (!COUNT) {
-                float4* px = image + (size_t)ly * W + lx;
-                f3 acc;
-                if (sd.renderedFramesCount == 0) { /* :318 */
-                    acc = result;
-                } else {
-                    const float4 o = *px;                                             /* :314 */
-                    const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u); /* :316 */
-                    const float iw = 1.0f - weight;
-                    acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight, o.z * iw + result.z * weight);
-                }
-                store_pixel(image, wire, wire_ch, (size_t)ly * W + lx, acc); /* :323 */
-            }
-            if (COUNT) cnt.pixels++;
-            active = false;
-        }
-    }
-}
-
-template <bool COUNT, bool DIAG, int SK, bool PAIRS>
-__global__ __launch_bounds__(64, 4) void pt_megakernel_regen(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
-                                                         const wcpt_sphere* __restrict__ spheres,
-                                                         const wcpt_draw_command* __restrict__ draws,
-                                                         const uint64_t* __restrict__ tri_records,
-                                                         float4* __restrict__ image, float* __restrict__ wire,
-                                                         uint32_t wire_ch, uint32_t W, uint32_t H,
-                                                         uint32_t y0, uint32_t rows, uint32_t tilesX, uint32_t total,
-                                                         uint32_t* __restrict__ heads, uint32_t parity, uint32_t refill,
-                                                         uint32_t* __restrict__ status,
-                                                         unsigned long long* __restrict__ counters)
-{
-    if (blockIdx.x == 0 && threadIdx.x == 0) heads[parity ^ 1u] = 0u; /* the next launch's queue */
-    uint32_t* head = heads + parity;
-    Counters cnt = {};
-    bool overflow = false;
-    if constexpr (SK == 0) {
-        uint64_t mem[kPrivateStack];
-        PrivateStack<kPrivateStack> stk;
-        stk.mem = (priv_u64_ptr)mem;
-        regen_loop<COUNT, DIAG, PAIRS>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, rows, tilesX, total,
-                                       head, refill, stk, cnt, overflow);
-    } else {
-        __shared__ uint64_t s_stack[kLdsStack * 64];
-        uint64_t spill[kSpillStack];
-        LdsStack<kLdsStack, kSpillStack> stk;
-        stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
-        stk.spill = (priv_u64_ptr)spill;
-        regen_loop<COUNT, DIAG, PAIRS>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, rows, tilesX, total,
-                                       head, refill, stk, cnt, overflow);
-    }
-    if (overflow) atomicOr(status, 1u);
-    flush_counters<COUNT>(cnt, counters);
-}
-
 /* Derived triangle records (pt_device.h), single and pair formats: one thread per pair. Same subtractions as
  * rayTriangle (:122-123). The second slot of the last pair of an odd count is zero (never inside a leaf's
  * range: leaf_record bounds leaves by the triangle count). */
@@ -340,41 +220,19 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
 template <bool COUNT, bool DIAG, int SK, bool PAIRS>
 static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
 {
-    if (a.mk_regen == 0) {
-        /* scattered tile order: block b renders tile (b * m) mod tiles for an m coprime with tiles near 0.618 * tiles,
-         * so the tiles resident on one CU at once come from all over the frame */
-        uint32_t scatter = 0;
-        const bool one_round = (uint64_t)tiles <= 16ull * (uint64_t)mk.cus; /* <= ~4 resident waves per SIMD */
-        if ((a.mk_tile_order == 1 || (a.mk_tile_order == 2 && one_round)) && tiles > 2) {
-            uint32_t m = (uint32_t)((uint64_t)tiles * 618034u / 1000000u) | 1u;
-            auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t r = x % y; x = y; y = r; } return x; };
-            while (gcd(m, tiles) != 1u) m += 2u;
-            scatter = m;
-        }
-        hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS>), dim3(tiles), dim3(64), 0, stream, a.sd,
-                           a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H, a.y0,
-                           a.rows, tilesX, tiles, scatter, a.status, a.counters);
-        return hipGetLastError();
+    /* scattered tile order: block b renders tile (b * m) mod tiles for an m coprime with tiles near 0.618 * tiles,
+     * so the tiles resident on one CU at once come from all over the frame */
+    uint32_t scatter = 0;
+    const bool one_round = (uint64_t)tiles <= 16ull * (uint64_t)mk.cus; /* <= ~4 resident waves per SIMD */
+    if ((a.mk_tile_order == 1 || (a.mk_tile_order == 2 && one_round)) && tiles > 2) {
+        uint32_t m = (uint32_t)((uint64_t)tiles * 618034u / 1000000u) | 1u;
+        auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t r = x % y; x = y; y = r; } return x; };
+        while (gcd(m, tiles) != 1u) m += 2u;
+        scatter = m;
     }
-    /* persistent grid: at most the resident waves of the chip, and at most ceil(tiles / mk_regen) waves, so each
-     * lane regenerates about mk_regen or more pixels */
-    auto kern = dev::pt_megakernel_regen<COUNT, DIAG, SK, PAIRS>;
-    int& bpc = mk.bpc[COUNT ? 1 : 0][SK][PAIRS ? 1 : 0];
-    if (bpc == 0) {
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, 64, 0);
-        if (e != hipSuccess) return e;
-        if (bpc < 1) bpc = 1;
-    }
-    const uint64_t resident = (uint64_t)bpc * (uint64_t)mk.cus;
-    const uint64_t want = ((uint64_t)tiles + a.mk_regen - 1u) / a.mk_regen;
-    uint32_t grid = (uint32_t)(want < resident ? want : resident);
-    if (const char* g = getenv("WCPT_MK_GRID")) grid = (uint32_t)atoi(g); /* experiments (tools/ab.py) */
-    if (getenv("WCPT_MK_TRACE")) fprintf(stderr, "regen grid %u (bpc %d, cus %d, tiles %u)\n", grid, bpc, mk.cus, tiles);
-    const uint32_t refill = a.mk_refill < 1u ? 1u : (a.mk_refill > 64u ? 64u : a.mk_refill);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, stream, a.sd, a.materials, a.spheres, a.draws, a.tri_records,
-                       a.image, a.wire, a.wire_ch, a.W, a.H, a.y0, a.rows, tilesX, tiles * 64u, mk.head, mk.parity, refill, a.status,
-                       a.counters);
-    mk.parity ^= 1u;
+    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS>), dim3(tiles), dim3(64), 0, stream, a.sd,
+                       a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H, a.y0,
+                       a.rows, tilesX, tiles, scatter, a.status, a.counters);
     return hipGetLastError();
 }
 
@@ -404,8 +262,6 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
         if (e == hipSuccess) e = hipDeviceGetAttribute(&mk.cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
     }
-    if (a.mk_regen != 0 && (uint64_t)tiles * 64u >= (1ull << 32)) return hipErrorInvalidValue;
-    if (a.mk_regen != 0 && !mk.head) return hipErrorInvalidValue;
     if (a.pair_records) return launch_mega_sk<true>(a, mode, stack_kind, mk, stream, tilesX, tiles);
     return launch_mega_sk<false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
 }

@@ -94,11 +94,11 @@ struct wcpt_context {
     uint32_t* d_status = nullptr;
     unsigned long long* d_counters = nullptr;
     wcpt::WfState wf;                  /* path state of the wavefront kernels (allocated on first use) */
-    wcpt::MkState mk;                  /* pixel queue heads of the regenerating megakernel */
+    wcpt::MkState mk;                  /* megakernel launch state (CU count) */
     uint32_t* d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
-    int stack_kind = 0;                /* WCPT_OPTION_STACK: 0 scratch (default; measured faster on c2), 1 LDS + spill */
+    int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + spill (default; c2 -2%, 135-row blocks -8%) */
     int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
@@ -106,8 +106,6 @@ struct wcpt_context {
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (measured optimum 8..16 on c3) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
-    int mk_regen = 0;                  /* WCPT_OPTION_MK_REGEN */
-    int mk_refill = 16;                /* WCPT_OPTION_MK_REFILL */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
     std::vector<TriRecords> tri;       /* per draw command index */
@@ -341,8 +339,6 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.tri_records = nullptr;
     a.pair_records = false;
     a.wf_refill = (uint32_t)ctx->wf_refill;
-    a.mk_regen = (uint32_t)ctx->mk_regen;
-    a.mk_refill = (uint32_t)ctx->mk_refill;
     a.mk_tile_order = (uint32_t)ctx->mk_tile_order;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ctx->profiling && mode == wcpt::kModeRender) {
@@ -432,8 +428,6 @@ int wcpt_create(int device, wcpt_context** out_ctx)
     if (e == hipSuccess) e = hipMalloc(&ctx->d_status, 4);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_counters, kNumCounters * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(ctx->d_status, 0, 4);
-    if (e == hipSuccess) e = hipMalloc(&ctx->mk.head, 2 * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(ctx->mk.head, 0, 2 * sizeof(uint32_t));
     if (e != hipSuccess) {
         int rc = hip_fail(nullptr, e, "wcpt_create");
         wcpt_destroy(ctx);
@@ -454,7 +448,6 @@ int wcpt_destroy(wcpt_context* ctx)
     if (ctx->own_image) (void)hipFree(ctx->own_image);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
-    if (ctx->mk.head) (void)hipFree(ctx->mk.head);
     wcpt::wf_release(ctx->wf);
     for (auto& t : ctx->tri)
         if (t.mem) (void)hipFree(t.mem);
@@ -497,14 +490,6 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     case WCPT_OPTION_WF_REFILL:
         if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
         ctx->wf_refill = value;
-        return WCPT_SUCCESS;
-    case WCPT_OPTION_MK_REGEN:
-        if (value < 0 || value > 1024) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "megakernel regeneration %d", value);
-        ctx->mk_regen = value;
-        return WCPT_SUCCESS;
-    case WCPT_OPTION_MK_REFILL:
-        if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
-        ctx->mk_refill = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_MK_TILE_ORDER:
         if (value < 0 || value > 2) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "tile order %d", value);

@@ -48,9 +48,7 @@ OPTION_TRIANGLE_CACHE = 5
 OPTION_PAIR_RECORDS = 6
 OPTION_PACKED_REFS = 7
 OPTION_WF_REFILL = 8
-OPTION_MK_REGEN = 9
-OPTION_MK_REFILL = 10
-OPTION_MK_TILE_ORDER = 11
+OPTION_MK_TILE_ORDER = 9
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
