@@ -1,0 +1,66 @@
+"""Load balance of the N-way row-block split on ONE GPU: every rank's block of a bench config rendered in turn
+(same kernel, options and progressive frames as bench.py), timed with HIP events on the context stream.
+
+    python tools/block_balance.py [--config c2] [--ns 2,4,8] [--frames 20] [--rounds 3]
+
+Per N prints each block's median ms/frame, the max (what the N-GPU step waits for), the mean, and
+full-frame / N (perfect split). max / (full / N) is the load-balance + tail loss of the split.
+"""
+import argparse
+import os
+
+import torch  # noqa: F401  (bench.py's load order: libwcpt binds to torch's HIP runtime)
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "wc-path-tracer_amd"), ROOT]
+
+import wcpt  # noqa: E402
+from wcpt import scene as wscene  # noqa: E402
+from wcpt.dist import row_block  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--ns", default="2,4,8")
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
+    s = wscene.generate(name)
+    ctx = wcpt.Context(0)
+    ctx.set_kernel(bench.DEFAULT_KERNEL[a.config])
+    dev = wcpt.DeviceScene(ctx, s)
+    ctx.create_screen(W, H)
+    sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
+
+    def timed(y0, rows):
+        ctx.set_row_range(y0, rows)
+        for sd in sds[:3]:
+            ctx.render(sd, *dev.addresses())
+        out = []
+        for _ in range(a.rounds):
+            ctx.profile_begin()
+            for sd in sds:
+                ctx.render(sd, *dev.addresses())
+            ms, n = ctx.profile_end()
+            ctx.sync()
+            out.append(ms / n)
+        return statistics.median(out)
+
+    full = timed(0, H)
+    print(f"{a.config}: {desc}; full frame {full:.4f} ms", flush=True)
+    for n in [int(x) for x in a.ns.split(",")]:
+        t = [timed(*row_block(H, n, r)) for r in range(n)]
+        mx, mean = max(t), sum(t) / n
+        print(f"N={n}: blocks {' '.join(f'{x:.4f}' for x in t)} | max {mx:.4f} mean {mean:.4f} full/N {full / n:.4f} "
+              f"| max/(full/N) {mx / (full / n):.2f} max/mean {mx / mean:.2f}", flush=True)
+    dev.free()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
