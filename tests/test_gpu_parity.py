@@ -638,6 +638,52 @@ def test_scattered_tile_order_matches_oracle(gpu_ctx, name, W, H, bounces, spp, 
     assert cnt == rcnt
 
 
+@pytest.mark.parametrize("pipes", [2, 3, 4])
+@pytest.mark.parametrize("name,W,H,bounces,spp,frame,rows", [
+    ("cornell", 67, 45, 4, 3, 0, None),     # ragged, several samples per pixel
+    ("atrium", 96, 54, 4, 1, 2, None),
+    ("default_dielectric", 48, 40, 3, 2, 7, None),
+    ("atrium", 200, 120, 4, 1, 1, 40),      # a row block
+    ("cornell", 24, 8, 2, 1, 0, None),      # 3 tiles: fewer tiles than pipelines at 4
+])
+def test_wavefront_pipelines_match_oracle(gpu_ctx, pipes, name, W, H, bounces, spp, frame, rows):
+    """WCPT_OPTION_WF_PIPES = K: K wavefront pipelines on K streams (tile t in pipeline t % K) render exactly the
+    oracle's image and count exactly its work."""
+    s = get_scene(name)
+    init = np.random.default_rng(9).uniform(0, 1, (rows or H, W, 4)).astype(np.float32)
+    y0 = (H - rows) // 2 if rows else 0
+    gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, pipes)
+    try:
+        img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, y0=y0, rows=rows, init=init,
+                              kernel=wcpt.KERNEL_WAVEFRONT)
+        img2, _ = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, y0=y0, rows=rows, init=init,
+                             kernel=wcpt.KERNEL_WAVEFRONT)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, 1)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, y0=y0, rows=rows,
+                                    image=init, threads=8)
+    assert_close(img, ref)
+    assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
+    assert cnt == rcnt
+
+
+def test_wavefront_pipelines_full_frame(gpu_ctx):
+    """1080p atrium frame: 2 and 4 pipelines give the bit-identical frame of one pipeline, and the stream join
+    orders a following readback after every pipeline."""
+    s = get_scene("atrium")
+    W, H = 1920, 1080
+    init = np.zeros((H, W, 4), np.float32)
+    one, c1 = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=0, init=init, kernel=wcpt.KERNEL_WAVEFRONT)
+    for k in (2, 4):
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, k)
+        try:
+            img, ck = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=0, init=init, kernel=wcpt.KERNEL_WAVEFRONT)
+        finally:
+            gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, 1)
+        assert np.array_equal(img.view(np.uint32), one.view(np.uint32))
+        assert ck == c1
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("channels", [3, 4])
 def test_gather_output_equals_image(gpu_ctx, kernel, channels):

@@ -2,7 +2,7 @@
 
     python tools/ab.py --config c3 --variants "kernel=0" "kernel=2" "kernel=2,deindex=1" [--frames 5 --rounds 3]
 
-Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, order=<0|1|2>, deindex=<0|1> (mesh re-laid out in
+Each variant is a comma list of option=value: stack=<0|1>, kernel=<0|2>, order=<0|1|2>, pipes=<1..4>, deindex=<0|1> (mesh re-laid out in
 BVH leaf order with identity indices: same triangles, same results, soup-like locality). Prints the median
 ms/frame (HIP events on the context stream) and Mray/s.
 """
@@ -68,6 +68,7 @@ def main():
             ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, int(o.get("refs", 1)))
             ctx.set_option(wcpt._lib.OPTION_WF_REFILL, int(o.get("refill", 12)))
             ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, int(o.get("order", 2)))
+            ctx.set_option(wcpt._lib.OPTION_WF_PIPES, int(o.get("pipes", 1)))
             dev = scenes[o.get("deindex", "0")]
             ctx.profile_begin()
             for sd in sds:

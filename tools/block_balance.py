@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--ns", default="2,4,8")
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--first", action="store_true", help="rank 0's block only (a size sweep)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
@@ -54,8 +55,8 @@ def main():
     full = timed(0, H)
     print(f"{a.config}: {desc}; full frame {full:.4f} ms", flush=True)
     for n in [int(x) for x in a.ns.split(",")]:
-        t = [timed(*row_block(H, n, r)) for r in range(n)]
-        mx, mean = max(t), sum(t) / n
+        t = [timed(*row_block(H, n, r)) for r in range(1 if a.first else n)]
+        mx, mean = max(t), sum(t) / len(t)
         print(f"N={n}: blocks {' '.join(f'{x:.4f}' for x in t)} | max {mx:.4f} mean {mean:.4f} full/N {full / n:.4f} "
               f"| max/(full/N) {mx / (full / n):.2f} max/mean {mx / mean:.2f}", flush=True)
     dev.free()

@@ -74,6 +74,18 @@ struct WfState {
     int trace_bpc[3][2][3] = {};   /* trace-kernel blocks per CU by (mode, single draw, LDS stack variant)  */
 };
 
+/* Concurrent wavefront pipelines (WCPT_OPTION_WF_PIPES): pipeline j of K owns the 8x8 tiles t with t % K == j and
+ * runs its own init / trace / shade sequence on its own stream (pipeline 0 on the context's stream), so the tail of
+ * one pipeline's trace (a few slow rays on an otherwise idle chip) overlaps the bulk of another's. Paths never
+ * interact, so the image and the counters are those of one pipeline. */
+constexpr int kWfMaxPipes = 4;
+struct WfPipes {
+    WfState pipe[kWfMaxPipes];
+    hipStream_t aux[kWfMaxPipes] = {};   /* [1..K-1]: created on first use, on the context's device */
+    hipEvent_t fork = nullptr;
+    hipEvent_t join[kWfMaxPipes] = {};
+};
+
 /* Megakernel launch state, per context. */
 struct MkState {
     int cus = 0;               /* CU count of the context's device (0 = not yet queried) */
@@ -93,10 +105,12 @@ hipError_t launch_composite(const float4* img, uint64_t pixels, void* dst, bool 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream);
 /* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
 /* lds_stack: LDS traversal-stack entries per lane of the trace kernel (10, 16 or 24; render mode only). */
-hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, int lds_stack,
+/* pipes: concurrent pipelines (1..kWfMaxPipes; sorting and diagnostics use 1). */
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes, bool sort_rays, int lds_stack,
                             hipStream_t stream);
 hipError_t wf_reserve(WfState& s, uint32_t paths);
 void wf_release(WfState& s);
+void wf_release(WfPipes& w);
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n,
                            hipStream_t stream);
 

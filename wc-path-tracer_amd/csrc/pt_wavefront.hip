@@ -34,7 +34,11 @@
 namespace wcpt {
 namespace dev {
 
-constexpr uint32_t kTraceChunk = 64;   /* queue entries a wave claims per atomicAdd */
+/* Queue entries a wave claims per atomicAdd. */
+#ifndef WCPT_TRACE_CHUNK
+#define WCPT_TRACE_CHUNK 64
+#endif
+constexpr uint32_t kTraceChunk = WCPT_TRACE_CHUNK;
 constexpr int kShadeBlock = 256;
 
 
@@ -106,7 +110,7 @@ template <bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
                                                        WfBuffers b, float4* __restrict__ image,
                                                        uint32_t W, uint32_t H, uint32_t y0, uint32_t rows,
-                                                       uint32_t tilesX, uint32_t total,
+                                                       uint32_t tilesX, uint32_t total, uint32_t pipe, uint32_t npipes,
                                                        unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_wave[kShadeBlock / 64], s_base;
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
         float rt = kInfinity;
         Ray ray;
         if (w < total) {
-            const uint32_t t = w >> 6, q = w & 63u;           /* 8x8 tiles: coherent initial queue */
+            const uint32_t t = (w >> 6) * npipes + pipe, q = w & 63u; /* 8x8 tiles (this pipeline's): coherent initial queue */
             const uint32_t lx = (t % tilesX) * 8u + (q & 7u);
             const uint32_t ly = (t / tilesX) * 8u + (q >> 3);
             if (lx < W && ly < rows) {
@@ -229,7 +233,16 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
 
     bool has = false, drained = false;
-    uint32_t lo = 0, hi = 0; /* this wave's claimed queue range [lo, hi) (wave-uniform) */
+    /* this wave's claimed queue range [lo, hi) (wave-uniform). The first chunk is static (chunk blockIdx.x), so a
+     * launch with fewer rays than resident waves costs no atomics for the waves without work: same-address
+     * device-scope atomics serialise, and one per wave of the persistent grid cost ~0.28 ms per launch. Later
+     * chunks come from the global head, which counts past the grid's static chunks. */
+    const uint32_t static_end = gridDim.x * kTraceChunk;
+    uint32_t lo = blockIdx.x * kTraceChunk, hi = min(lo + kTraceChunk, n);
+    if (lo >= n) {
+        lo = hi = 0;
+        drained = true;
+    }
     uint32_t p = 0, d = 0, prim = kNoPrim, primDraw = 0;
     uint32_t ca = 0, cb = 0, cr = 0, mode = kModeDone;
     float rt = kInfinity;
@@ -262,7 +275,11 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             while (need) {
                 if (lo == hi) {
                     uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(b.head, kTraceChunk);
+                    if (static_end >= n) { /* every chunk was static */
+                        drained = true;
+                        break;
+                    }
+                    if (lane == 0) base = static_end + atomicAdd(b.head, kTraceChunk);
                     base = __builtin_amdgcn_readfirstlane(base); /* wave-uniform: keeps lo/hi in SGPRs */
                     if (base >= n) {
                         drained = true;
@@ -535,6 +552,17 @@ void wf_release(WfState& s)
     s = WfState{};
 }
 
+void wf_release(WfPipes& w)
+{
+    for (int j = 0; j < kWfMaxPipes; j++) {
+        wf_release(w.pipe[j]);
+        if (w.aux[j]) (void)hipStreamDestroy(w.aux[j]);
+        if (w.join[j]) (void)hipEventDestroy(w.join[j]);
+    }
+    if (w.fork) (void)hipEventDestroy(w.fork);
+    w = WfPipes{};
+}
+
 /* Ray sorting between bounces: key = direction octant (3 bits) | Morton code of the origin quantised to a
  * 512^3 grid over the first draw's root box (27 bits); queue slots at or past the live count get the sentinel
  * key 0xffffffff and sort to the end. Rays that start close together and head the same way then share a
@@ -629,41 +657,20 @@ static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b
                                               s.sort_order, (int)P, 0, 32, stream);
 }
 
-hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort_rays, int lds_stack, hipStream_t stream)
+/* One pipeline: init + samples*(maxBounce+1) trace/shade iterations over the tiles t with t % npipes == pipe. */
+static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, uint32_t pipe,
+                              uint32_t npipes, bool sort_rays, int ldsn, int cus, uint32_t trace_grid,
+                              uint32_t shade_grid, hipStream_t stream)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
-    const uint32_t tilesY = (a.rows + 7u) / 8u;
-    const uint64_t total64 = (uint64_t)tilesX * tilesY * 64ull;
-    if (total64 == 0) return hipSuccess;
-    if (total64 > 0xFFFFFFC0ull || (uint64_t)a.W * a.rows > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t total = (uint32_t)total64;
+    const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
+    if (pipe >= tiles) return hipSuccess;
+    const uint32_t total = ((tiles - pipe + npipes - 1u) / npipes) * 64u;
     const uint32_t P = a.W * a.rows;
     hipError_t e = wf_reserve(s, P);
     if (e != hipSuccess) return e;
-    int cus = 0;
-    e = cu_count(s, cus);
-    if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
     const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
-    const int ldsn = (lds_stack == 16 || lds_stack == 24) ? lds_stack : 10;
-    int& bpc = s.trace_bpc[mode][single ? 1 : 0][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
-    if (bpc == 0) {
-        e = wf_dispatch(mode, single, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);
-        if (e != hipSuccess) return e;
-        if (bpc < 1) bpc = 1;
-    }
-    const uint32_t trace_grid = (uint32_t)(bpc * cus);
-/* Shade blocks per CU (grid-stride over the queue). The continuing paths are appended in roughly the order
- * the blocks walk their chunks, so a small grid keeps the next queue close to the input order (coherent rays
- * for the next trace). Measured on c3: 4 -> 7.98 ms, 8 -> 8.13, 16 -> 8.56, 32 -> 8.98, one thread per slot ->
- * 8.97. */
-#ifndef WCPT_SHADE_BLOCKS_PER_CU
-#define WCPT_SHADE_BLOCKS_PER_CU 4
-#endif
-    /* 0: one thread per path slot (no grid-stride loop) */
-    const uint32_t shade_grid = WCPT_SHADE_BLOCKS_PER_CU > 0 ? (uint32_t)(cus * WCPT_SHADE_BLOCKS_PER_CU)
-                                                             : (P + dev::kShadeBlock - 1) / dev::kShadeBlock;
-
     e = hipMemsetAsync(s.ctr, 0, 4 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     WfBuffers b;
@@ -673,9 +680,9 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     b.hit = s.hit;
     b.order = nullptr;
     b.head = s.ctr + 2;
-    b.diag = s.diag;
+    b.diag = s0.diag;
     if (mode == kModeDiag) {
-        e = hipMemsetAsync(s.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
+        e = hipMemsetAsync(s0.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
     }
     b.wire = a.wire;
@@ -685,16 +692,15 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);
     if (count)
         hipLaunchKernelGGL(dev::wf_init<true>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
-                           a.W, a.H, a.y0, a.rows, tilesX, total, a.counters);
+                           a.W, a.H, a.y0, a.rows, tilesX, total, pipe, npipes, a.counters);
     else
         hipLaunchKernelGGL(dev::wf_init<false>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
-                           a.W, a.H, a.y0, a.rows, tilesX, total, a.counters);
+                           a.W, a.H, a.y0, a.rows, tilesX, total, pipe, npipes, a.counters);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     /* each iteration advances every live path by one segment; a path needs <= samples*(maxBounce+1) */
     uint64_t iters = (uint64_t)a.sd.samples * ((uint64_t)a.sd.maxBounceCount + 1ull);
     if (iters > (1ull << 20)) iters = 1ull << 20; /* bounded; WCPT documents the cap */
-    sort_rays = sort_rays && a.sd.drawCommandCount > 0;
     for (uint64_t it = 0; it < iters; it++) {
         b.order = nullptr;
         if (sort_rays && it > 0) { /* bounce rays; the primary queue is already in 8x8-tile order */
@@ -709,6 +715,79 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfState& s, bool sort
         std::swap(b.count_in, b.count_out);
     }
     return hipSuccess;
+}
+
+hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes, bool sort_rays, int lds_stack,
+                            hipStream_t stream)
+{
+    const uint32_t tilesX = (a.W + 7u) / 8u;
+    const uint32_t tilesY = (a.rows + 7u) / 8u;
+    const uint64_t total64 = (uint64_t)tilesX * tilesY * 64ull;
+    if (total64 == 0) return hipSuccess;
+    if (total64 > 0xFFFFFFC0ull || (uint64_t)a.W * a.rows > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    WfState& s0 = w.pipe[0];
+    int cus = 0;
+    hipError_t e = cu_count(s0, cus);
+    if (e != hipSuccess) return e;
+    const bool single = a.sd.drawCommandCount == 1;
+    const int ldsn = (lds_stack == 16 || lds_stack == 24) ? lds_stack : 10;
+    int& bpc = s0.trace_bpc[mode][single ? 1 : 0][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
+    if (bpc == 0) {
+        e = wf_dispatch(mode, single, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);
+        if (e != hipSuccess) return e;
+        if (bpc < 1) bpc = 1;
+    }
+    const uint32_t trace_grid = (uint32_t)(bpc * cus);
+/* Shade blocks per CU (grid-stride over the queue). The continuing paths are appended in roughly the order
+ * the blocks walk their chunks, so a small grid keeps the next queue close to the input order (coherent rays
+ * for the next trace). Measured on c3: 4 -> 7.98 ms, 8 -> 8.13, 16 -> 8.56, 32 -> 8.98, one thread per slot ->
+ * 8.97. */
+#ifndef WCPT_SHADE_BLOCKS_PER_CU
+#define WCPT_SHADE_BLOCKS_PER_CU 4
+#endif
+    /* 0: one thread per path slot (no grid-stride loop) */
+    const uint32_t P = a.W * a.rows;
+    const uint32_t shade_grid = WCPT_SHADE_BLOCKS_PER_CU > 0 ? (uint32_t)(cus * WCPT_SHADE_BLOCKS_PER_CU)
+                                                             : (P + dev::kShadeBlock - 1) / dev::kShadeBlock;
+    sort_rays = sort_rays && a.sd.drawCommandCount > 0;
+    uint32_t K = (uint32_t)(pipes < 1 ? 1 : (pipes > kWfMaxPipes ? kWfMaxPipes : pipes));
+    if (sort_rays || mode == kModeDiag) K = 1; /* one sort scratch and one diagnostics block */
+    const uint32_t tiles = tilesX * tilesY;
+    if (K > tiles) K = tiles;
+    if (K == 1) return launch_pipe(a, mode, s0, s0, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream);
+
+    /* fork: pipelines 1..K-1 run on their own streams after everything already queued on the context's stream */
+    if (!w.fork) {
+        e = hipEventCreateWithFlags(&w.fork, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    for (uint32_t j = 1; j < K; j++) {
+        if (!w.aux[j]) {
+            e = hipStreamCreateWithFlags(&w.aux[j], hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+        }
+        if (!w.join[j]) {
+            e = hipEventCreateWithFlags(&w.join[j], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+    }
+    e = hipEventRecord(w.fork, stream);
+    if (e != hipSuccess) return e;
+    for (uint32_t j = 1; j < K; j++) {
+        e = hipStreamWaitEvent(w.aux[j], w.fork, 0);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t first = hipSuccess;
+    for (uint32_t j = 0; j < K && first == hipSuccess; j++)
+        first = launch_pipe(a, mode, w.pipe[j], s0, j, K, false, ldsn, cus, trace_grid, shade_grid,
+                            j == 0 ? stream : w.aux[j]);
+    /* join: the context's stream continues after every pipeline (also after a failed enqueue) */
+    for (uint32_t j = 1; j < K; j++) {
+        e = hipEventRecord(w.join[j], w.aux[j]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, w.join[j], 0);
+        if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    return first;
 }
 
 } // namespace wcpt

@@ -93,7 +93,7 @@ struct wcpt_context {
     bool sharded = false;
     uint32_t* d_status = nullptr;
     unsigned long long* d_counters = nullptr;
-    wcpt::WfState wf;                  /* path state of the wavefront kernels (allocated on first use) */
+    wcpt::WfPipes wf;                  /* path state + streams of the wavefront pipelines (allocated on first use) */
     wcpt::MkState mk;                  /* megakernel launch state (CU count) */
     uint32_t* d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
@@ -105,6 +105,7 @@ struct wcpt_context {
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (measured optimum 8..16 on c3) */
+    int wf_pipes = 1;                  /* WCPT_OPTION_WF_PIPES */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
@@ -359,7 +360,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
     case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->mk, ctx->stream); break;
-    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream); break;
+    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->wf_pipes, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream); break;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
@@ -490,6 +491,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     case WCPT_OPTION_WF_REFILL:
         if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
         ctx->wf_refill = value;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_WF_PIPES:
+        if (value < 1 || value > wcpt::kWfMaxPipes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pipelines %d", value);
+        ctx->wf_pipes = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_MK_TILE_ORDER:
         if (value < 0 || value > 2) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "tile order %d", value);
@@ -812,8 +817,8 @@ int wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n)
     if (rc) return rc;
     if (!out || n > 8) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_read_diagnostics: bad output");
     memset(out, 0, sizeof(uint64_t) * n);
-    if (!ctx->wf.diag || n == 0) return WCPT_SUCCESS;
-    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wf.diag, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream),
+    if (!ctx->wf.pipe[0].diag || n == 0) return WCPT_SUCCESS;
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wf.pipe[0].diag, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream),
             "hipMemcpyAsync(diag)");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     return WCPT_SUCCESS;
