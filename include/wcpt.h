@@ -82,7 +82,7 @@ extern "C" {
  * tiles resident on a CU at once come from all over the frame; 2 (default) scattered when the launch fits in about
  * one round of resident waves (small row blocks: the tail is the most loaded CU), banded otherwise. Same results. */
 #define WCPT_OPTION_MK_TILE_ORDER 9
-/* Wavefront: concurrent pipelines (1..4, default 1). Pipeline j renders the 8x8 tiles t with t % K == j on its own
+/* Wavefront: concurrent pipelines (1..4, default 2). Pipeline j renders the 8x8 tiles t with t % K == j on its own
  * stream, so one pipeline's trace tail (a few slow rays) overlaps another's bulk. Same results. */
 #define WCPT_OPTION_WF_PIPES 10
 

@@ -638,7 +638,7 @@ def test_scattered_tile_order_matches_oracle(gpu_ctx, name, W, H, bounces, spp, 
     assert cnt == rcnt
 
 
-@pytest.mark.parametrize("pipes", [2, 3, 4])
+@pytest.mark.parametrize("pipes", [1, 2, 3, 4])
 @pytest.mark.parametrize("name,W,H,bounces,spp,frame,rows", [
     ("cornell", 67, 45, 4, 3, 0, None),     # ragged, several samples per pixel
     ("atrium", 96, 54, 4, 1, 2, None),
@@ -659,7 +659,7 @@ def test_wavefront_pipelines_match_oracle(gpu_ctx, pipes, name, W, H, bounces, s
         img2, _ = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, y0=y0, rows=rows, init=init,
                              kernel=wcpt.KERNEL_WAVEFRONT)
     finally:
-        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, 1)
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, wcpt._lib.DEFAULT_WF_PIPES)
     ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, y0=y0, rows=rows,
                                     image=init, threads=8)
     assert_close(img, ref)
@@ -673,13 +673,17 @@ def test_wavefront_pipelines_full_frame(gpu_ctx):
     s = get_scene("atrium")
     W, H = 1920, 1080
     init = np.zeros((H, W, 4), np.float32)
-    one, c1 = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=0, init=init, kernel=wcpt.KERNEL_WAVEFRONT)
+    gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, 1)
+    try:
+        one, c1 = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=0, init=init, kernel=wcpt.KERNEL_WAVEFRONT)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, wcpt._lib.DEFAULT_WF_PIPES)
     for k in (2, 4):
         gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, k)
         try:
             img, ck = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=0, init=init, kernel=wcpt.KERNEL_WAVEFRONT)
         finally:
-            gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, 1)
+            gpu_ctx.set_option(wcpt._lib.OPTION_WF_PIPES, wcpt._lib.DEFAULT_WF_PIPES)
         assert np.array_equal(img.view(np.uint32), one.view(np.uint32))
         assert ck == c1
 

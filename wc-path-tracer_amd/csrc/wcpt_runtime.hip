@@ -105,7 +105,7 @@ struct wcpt_context {
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (measured optimum 8..16 on c3) */
-    int wf_pipes = 1;                  /* WCPT_OPTION_WF_PIPES */
+    int wf_pipes = 2;                  /* WCPT_OPTION_WF_PIPES (2: c3 -2%, a c4 8-way row block -10%) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */

@@ -50,6 +50,7 @@ OPTION_PACKED_REFS = 7
 OPTION_WF_REFILL = 8
 OPTION_MK_TILE_ORDER = 9
 OPTION_WF_PIPES = 10
+DEFAULT_WF_PIPES = 2  # wcpt_runtime.hip
 
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
