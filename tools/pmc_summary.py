@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--config", default=None)
     ap.add_argument("--kernel-id", type=int, default=0)
+    ap.add_argument("--per-frame", type=int, default=2,
+                    help="dispatches of --frame-kernel per frame (wavefront: one wf_init per pipeline; "
+                         "WCPT_OPTION_WF_PIPES defaults to 2)")
     ap.add_argument("--frame-kernel", default=None,
                     help="whole-frame mode (wavefront: several kernels per frame): --kernel is a comma list of "
                          "kernel filters whose counters are SUMMED over all their dispatches and divided by the "
@@ -38,7 +41,7 @@ def main():
     per = load(a.dir)
     out = {}
     if a.frame_kernel:
-        frames = sum(len(next(iter(c.values()))) for n, c in per.items() if a.frame_kernel in n)
+        frames = sum(len(next(iter(c.values()))) for n, c in per.items() if a.frame_kernel in n) // a.per_frame
         if not frames:
             raise SystemExit(f"no dispatches of {a.frame_kernel} in {a.dir}")
         filters = a.kernel.split(",")
