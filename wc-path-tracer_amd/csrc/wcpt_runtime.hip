@@ -104,7 +104,7 @@ struct wcpt_context {
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
-    int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (measured optimum 8..16 on c3) */
+    int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (c3: 12 -> 6.83 ms, 20..32 -> 6.73, 48 -> 7.03) */
     int wf_pipes = 2;                  /* WCPT_OPTION_WF_PIPES (2: c3 -2%, a c4 8-way row block -10%) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
