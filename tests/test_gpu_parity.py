@@ -541,7 +541,7 @@ def test_stack_refs_match_oracle(gpu_ctx, kernel, refs):
         gpu_ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, 1)
 
 
-@pytest.mark.parametrize("refill", [1, 12, 64])
+@pytest.mark.parametrize("refill", [1, 12, 20, 64])
 def test_wavefront_refill_thresholds(gpu_ctx, refill):
     """The wavefront trace's refill threshold changes only the order rays are processed in."""
     s = get_scene("atrium")
@@ -549,7 +549,7 @@ def test_wavefront_refill_thresholds(gpu_ctx, refill):
     try:
         img, cnt = gpu_render(gpu_ctx, s, 80, 48, bounces=4, kernel=wcpt.KERNEL_WAVEFRONT)
     finally:
-        gpu_ctx.set_option(wcpt._lib.OPTION_WF_REFILL, 12)
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_REFILL, wcpt._lib.DEFAULT_WF_REFILL)
     ref, rcnt = oracle.render_scene(s, 80, 48, max_bounce=4, threads=8)
     assert_close(img, ref)
     assert cnt == rcnt
