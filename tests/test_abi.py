@@ -32,6 +32,19 @@ def test_abi_version():
     assert wcpt.lib.wcpt_abi_version() == 1
 
 
+def test_option_and_kernel_constants_match_header():
+    """The Python mirror's option / kernel numbers are the header's (renumbering one side breaks callers)."""
+    text = open(HEADER).read()
+    options = dict(re.findall(r"#define WCPT_OPTION_(\w+)\s+(\d+)", text))
+    assert len(options) >= 9
+    for name, value in options.items():
+        assert getattr(wcpt._lib, "OPTION_" + name) == int(value), name
+    assert len(set(options.values())) == len(options), "duplicate option numbers"
+    kernels = dict(re.findall(r"#define WCPT_KERNEL_(\w+)\s+(\d+)", text))
+    for name, value in kernels.items():
+        assert getattr(wcpt, "KERNEL_" + name) == int(value), name
+
+
 def test_layouts_match_reference():
     """GLSL scalar layouts (pathTracer.comp:10-95) == Jai structs (PathTracingRenderer.jai:38-140)."""
     sd = wcpt.SCENE_DATA_DTYPE
