@@ -66,8 +66,11 @@ extern "C" {
 /* Derived triangle records. wcpt_render derives per draw command one 48-byte record per triangle (a, b-a, c-a)
  * from the draw's index and vertex buffers; leaf tests read them instead of index + vertex gathers (same
  * arithmetic, same results). 1 (default): rebuilt only when a draw's buffers were re-uploaded through
- * wcpt_buffer_upload / re-allocated, or its buffers or index count changed. 0: rebuilt on every render (use this
- * when the application writes vertex/index buffers by other means, e.g. its own kernels). */
+ * wcpt_buffer_upload / re-allocated, or its buffers or index count changed; the draw commands themselves are read
+ * from the context's host copy of what wcpt_buffer_upload wrote (bytes never uploaded are read from the device).
+ * 0: the draw commands are read from the device and the records rebuilt on every render (use this when the
+ * application writes draw-command, vertex or index buffers by other means, e.g. hipMemcpy to a
+ * wcpt_buffer_device_address or its own kernels: with 1, such writes into uploaded ranges are not seen). */
 #define WCPT_OPTION_TRIANGLE_CACHE 5
 /* Megakernel leaf tests: -1 (default) choose by mean triangles per leaf; 0 single records; 1 pair records
  * (two triangles per lane with packed-FP32 arithmetic). Results are identical either way. */
@@ -135,7 +138,11 @@ typedef struct wcpt_node {
 
 /* DrawCommand — pathTracer.comp:82-87 == PathTracingRenderer.jai:135-140. The array stride is the Jai
  * size_of = 32 bytes (28 bytes of fields + 4 bytes tail padding). The three fields are device
- * addresses from wcpt_buffer_device_address(). indexCount is not read by the kernel. */
+ * addresses from wcpt_buffer_device_address(). The reference's kernel never reads indexCount; this runtime does:
+ * it derives the triangle records from index positions [0, indexCount), so indexCount must not exceed the index
+ * buffer (checked for context buffers: wcpt_render returns WCPT_ERROR_INVALID_ARGUMENT), and vertex indices past a
+ * context vertex buffer give a triangle that is never hit. Write draw commands through wcpt_buffer_upload, or see
+ * WCPT_OPTION_TRIANGLE_CACHE. */
 typedef struct wcpt_draw_command {
     uint64_t vertexBuffer;          /* -> float[3] positions, stride 12 */
     uint64_t indexBuffer;           /* -> uint32 indices (BVH-permuted) */

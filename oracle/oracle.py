@@ -37,7 +37,9 @@ def _load():
     lib.oracle_pcg_hash.argtypes = [C.c_uint32]
     lib.oracle_rand.restype = f
     lib.oracle_rand.argtypes = [C.POINTER(C.c_uint32)]
-    for n in ("oracle_logf", "oracle_cosf", "oracle_expf"):
+    lib.oracle_libm_domain_mismatches.restype = C.c_uint64
+    lib.oracle_libm_domain_mismatches.argtypes = [C.c_uint32, C.c_uint32]
+    for n in ("oracle_logf", "oracle_cosf", "oracle_expf", "oracle_logf_rand", "oracle_cosf_2pi"):
         getattr(lib, n).restype = f
         getattr(lib, n).argtypes = [f]
     lib.oracle_random_direction.restype = None

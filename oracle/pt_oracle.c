@@ -11,7 +11,8 @@
  *   - src/shaders/include/constants.glsl:4-9   (bias, kInfinity, PI)
  *   - src/PathTracingRenderer.jai:147-217      (UpdateNodeBounds / Subdivide midpoint BVH)
  * with GLSL 4.50 built-ins written out: dot = (x*x' + y*y') + z*z'; cross per the GLSL spec;
- * normalize(v) = v / sqrt(dot(v,v)); reflect(I,N) = I - (2*dot(N,I))*N; refract per the GLSL spec;
+ * normalize(v) = v / sqrt(dot(v,v)) where vector / scalar = v * (1/s) (see div3s); reflect(I,N) =
+ * I - (2*dot(N,I))*N; refract per the GLSL spec;
  * mix(x,y,a) = x*(1-a) + y*a; sign(0) = 0; min/max = IEEE minNum/maxNum (a NaN operand yields the other).
  * log/cos/exp are the deterministic definitions of wc-path-tracer_amd/csrc/wcpt_libm.h (GLSL leaves their
  * precision to the driver; see DESIGN.md "Parity").
@@ -47,7 +48,9 @@ static inline v3 sub3(v3 a, v3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z);
 static inline v3 mul3(v3 a, v3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
 static inline v3 mul3s(v3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
 static inline v3 smul3(float s, v3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
-static inline v3 div3s(v3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
+/* GLSL vector / scalar, implemented as v * RN(1/s) (Vulkan allows 2.5 ULP for division; this is <= 1.5 ULP). The
+ * kernel evaluates the same expression with its correctly rounded reciprocal (pt_device.h operator/). */
+static inline v3 div3s(v3 a, float s) { const float r = 1.0f / s; return mk3(a.x * r, a.y * r, a.z * r); }
 static inline v3 sdiv3(float s, v3 a) { return mk3(s / a.x, s / a.y, s / a.z); }
 static inline float dot3(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline v3 cross3(v3 a, v3 b)
@@ -111,6 +114,23 @@ static inline v3 RandomDirection(uint32_t* seed)
 /* Exported for the libm / RNG known-answer tests. */
 float oracle_logf(float x) { return wcpt_logf(x); }
 float oracle_cosf(float x) { return wcpt_cosf(x); }
+/* the kernel's domain-specialised variants (equal to the general ones on rand()'s values / [0, 2*pi]) */
+float oracle_logf_rand(float x) { return wcpt_logf_rand(x); }
+float oracle_cosf_2pi(float x) { return wcpt_cosf_2pi(x); }
+/* Mismatches between the specialised and the general functions over the rand() outputs n * 2^-32 for
+ * n = first, first + stride, ... < 2^32 (log of the value, cos of 2*PI times it, Random.glsl:45-46). */
+uint64_t oracle_libm_domain_mismatches(uint32_t first, uint32_t stride)
+{
+    uint64_t bad = 0;
+    for (uint64_t n = first; n < (1ull << 32); n += stride) {
+        const float x = (float)(uint32_t)n * 2.3283064365386963e-10f;
+        const float th = 2.0f * 3.14159265358979323846264338327950288f * x;
+        const float l0 = wcpt_logf(x), l1 = wcpt_logf_rand(x);
+        const float c0 = wcpt_cosf(th), c1 = wcpt_cosf_2pi(th);
+        bad += (wcpt_f2u(l0) != wcpt_f2u(l1)) + (wcpt_f2u(c0) != wcpt_f2u(c1));
+    }
+    return bad;
+}
 float oracle_expf(float x) { return wcpt_expf(x); }
 void oracle_random_direction(uint32_t* seed, float* out3)
 {

@@ -1,0 +1,177 @@
+"""GPU tests of the C-ABI boundary's robustness (include/wcpt.h): draw commands written without
+wcpt_buffer_upload, draw commands whose indexCount exceeds the index buffer, vertex indices past the vertex
+buffer, and the range checks of buffer uploads / downloads.
+
+The reference (PathTracingRenderer.jai:251-256, BufferManager.jai:52-64) only ever fills its draw-command buffer
+through DBufferManager.Update; a host that writes device memory by other means must still get the frame its
+draw commands describe.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import wcpt
+from wcpt import scene as wscene
+import oracle
+
+from test_gpu_parity import assert_close, get_scene, _with_mesh
+
+pytestmark = pytest.mark.gpu
+
+_H2D = 1  # hipMemcpyHostToDevice
+
+
+def _hip():
+    """The HIP runtime instance libwcpt.so is bound to (the already-mapped library, not a second copy)."""
+    with open("/proc/self/maps") as f:
+        paths = sorted({ln.split()[-1] for ln in f if "libamdhip64.so" in ln})
+    if not paths:
+        pytest.fail("HIP runtime library not mapped")
+    h = C.CDLL(paths[0])
+    h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    h.hipMemcpy.restype = C.c_int
+    return h
+
+
+def _device_write(addr: int, arr: np.ndarray):
+    """hipMemcpy host -> device address, bypassing wcpt_buffer_upload (as an application kernel would)."""
+    arr = np.ascontiguousarray(arr)
+    assert _hip().hipMemcpy(C.c_void_p(addr), arr.ctypes.data, arr.nbytes, _H2D) == 0
+
+
+def _moved_positions(s, dx):
+    m = s.meshes[0]
+    return np.ascontiguousarray(m.positions + np.float32(dx), dtype=np.float32)
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_draw_commands_written_on_device_cache_off(gpu_ctx, kernel):
+    """Draw commands first uploaded for geometry A, then overwritten on the device (hipMemcpy) to point at a second
+    vertex buffer B. With WCPT_OPTION_TRIANGLE_CACHE = 0 the render reads the draw commands from the device and
+    derives the records from B: the frame equals the oracle's frame of B."""
+    s = get_scene("cornell")
+    W, H = 64, 48
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    posB = _moved_positions(s, 0.07)
+    bufB = gpu_ctx.buffer_from(posB)
+    gpu_ctx.set_kernel(kernel)
+    try:
+        gpu_ctx.create_screen(W, H)
+        sd = s.scene_data(W, H, max_bounce=3)
+        gpu_ctx.render(sd, *dev.addresses())          # geometry A: records derived and cached
+        gpu_ctx.sync()
+        draws = np.zeros(1, dtype=wcpt._lib.DRAW_COMMAND_DTYPE)
+        draws[0] = (gpu_ctx.buffer_address(bufB), gpu_ctx.buffer_address(dev.buffers[3]),
+                    gpu_ctx.buffer_address(dev.buffers[4]), s.meshes[0].indices.size, 0)
+        _device_write(dev.draws, draws)
+        gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 0)
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()
+        img = gpu_ctx.readback(H)
+        m = s.meshes[0]
+        ref, _ = oracle.render_scene(_with_mesh(s, wscene.HostBVH(posB, m.indices, m.nodes)), W, H, max_bounce=3,
+                                     threads=8)
+        assert_close(img, ref)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 1)
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        gpu_ctx.buffer_free(bufB)
+        dev.free()
+
+
+def test_draw_commands_never_uploaded_are_read_from_device(gpu_ctx):
+    """A draw-command buffer that was allocated but never written through wcpt_buffer_upload (its host copy holds
+    nothing) is read from the device even with the triangle cache on."""
+    s = get_scene("cornell")
+    W, H = 64, 48
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    dbuf = gpu_ctx.buffer_alloc(32)
+    try:
+        draws = np.zeros(1, dtype=wcpt._lib.DRAW_COMMAND_DTYPE)
+        draws[0] = (gpu_ctx.buffer_address(dev.buffers[2]), gpu_ctx.buffer_address(dev.buffers[3]),
+                    gpu_ctx.buffer_address(dev.buffers[4]), s.meshes[0].indices.size, 0)
+        _device_write(gpu_ctx.buffer_address(dbuf), draws)
+        gpu_ctx.create_screen(W, H)
+        sd = s.scene_data(W, H, max_bounce=3)
+        gpu_ctx.render(sd, dev.materials, dev.spheres, gpu_ctx.buffer_address(dbuf))
+        gpu_ctx.sync()
+        img = gpu_ctx.readback(H)
+        ref, _ = oracle.render_scene(s, W, H, max_bounce=3, threads=8)
+        assert_close(img, ref)
+    finally:
+        gpu_ctx.buffer_free(dbuf)
+        dev.free()
+
+
+def test_index_count_past_index_buffer_is_rejected(gpu_ctx):
+    s = get_scene("cornell")
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    try:
+        n = s.meshes[0].indices.size
+        draws = np.zeros(1, dtype=wcpt._lib.DRAW_COMMAND_DTYPE)
+        draws[0] = (gpu_ctx.buffer_address(dev.buffers[2]), gpu_ctx.buffer_address(dev.buffers[3]),
+                    gpu_ctx.buffer_address(dev.buffers[4]), n + 3, 0)
+        gpu_ctx.buffer_upload(dev.buffers[5], draws)
+        gpu_ctx.create_screen(32, 32)
+        with pytest.raises(wcpt.WcptError) as e:
+            gpu_ctx.render(s.scene_data(32, 32, max_bounce=1), *dev.addresses())
+        assert e.value.code == -1000 and "indexCount" in str(e.value)
+        # a valid indexCount renders again on the same context
+        draws[0]["indexCount"] = n
+        gpu_ctx.buffer_upload(dev.buffers[5], draws)
+        gpu_ctx.render(s.scene_data(32, 32, max_bounce=1), *dev.addresses())
+        gpu_ctx.sync()
+    finally:
+        dev.free()
+
+
+@pytest.mark.parametrize("pairs", [0, 1])
+def test_vertex_index_past_vertex_buffer_never_hits(gpu_ctx, pairs):
+    """An index past the vertex buffer (undefined in the reference) gives a triangle no ray accepts: the frame equals
+    the oracle's frame in which that triangle's vertex is NaN."""
+    rng = np.random.default_rng(11)
+    ntri = 24
+    pos = (rng.random((ntri * 3, 3), dtype=np.float32) * 2.0 - 1.0).astype(np.float32)
+    pos[:, 0] = pos[:, 0] * 0.25 + 1.5                 # in front of the default camera (looking along +x)
+    idx = np.arange(ntri * 3, dtype=np.uint32)
+    bad = 10                                           # triangle 10's second vertex index is out of range
+    idx_dev = idx.copy()
+    idx_dev[3 * bad + 1] = pos.shape[0] + 100000
+    lo, hi = pos.min(axis=0), pos.max(axis=0)
+    nodes = np.zeros(1, dtype=wcpt._lib.NODE_DTYPE)
+    nodes[0] = (lo, hi, 0, 3 * ntri)                   # one leaf
+    s = _with_mesh(get_scene("default"), wscene.HostBVH(pos, idx_dev, nodes))
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, pairs)
+    try:
+        W, H = 48, 40
+        gpu_ctx.create_screen(W, H)
+        sd = s.scene_data(W, H, max_bounce=2)
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()
+        img = gpu_ctx.readback(H)
+        pos_ref = np.concatenate([pos, np.full((1, 3), np.nan, np.float32)])
+        idx_ref = idx.copy()
+        idx_ref[3 * bad + 1] = pos.shape[0]
+        ref, _ = oracle.render_scene(_with_mesh(s, wscene.HostBVH(pos_ref, idx_ref, nodes)), W, H, max_bounce=2,
+                                     threads=8)
+        assert_close(img, ref)
+        full, _ = oracle.render_scene(_with_mesh(s, wscene.HostBVH(pos, idx, nodes)), W, H, max_bounce=2, threads=8)
+        assert (full != ref).any(), "the test triangle must be visible"
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, -1)
+        dev.free()
+
+
+def test_buffer_range_checks_do_not_wrap(gpu_ctx):
+    b = gpu_ctx.buffer_alloc(64)
+    try:
+        huge = (1 << 64) - 16
+        with pytest.raises(wcpt.WcptError):
+            gpu_ctx.buffer_download(b, 32, offset=huge)
+        with pytest.raises(wcpt.WcptError):
+            gpu_ctx.buffer_upload(b, np.zeros(32, np.uint8), offset=huge)
+        assert gpu_ctx.buffer_size(b) == 64             # no grow to a wrapped size
+    finally:
+        gpu_ctx.buffer_free(b)

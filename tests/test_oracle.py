@@ -68,6 +68,15 @@ def test_libm_accuracy(name, fn, ref, lo, hi):
     assert worst <= 2.0, f"{name}: worst error {worst:.2f} ulp"
 
 
+def test_libm_kernel_domains_equal_general():
+    """The kernel's wcpt_logf_rand / wcpt_cosf_2pi return the general functions' bits on every rand() output they
+    are called with (n * 2^-32, and 2*PI times it): checked on 2^32 / 251 values spread over the whole domain plus
+    its ends."""
+    assert oracle.lib.oracle_libm_domain_mismatches(0, 251) == 0
+    assert oracle.lib.oracle_libm_domain_mismatches(0xFFFFFF00, 1) == 0
+    assert oracle.lib.oracle_libm_domain_mismatches(0, 1 << 24) == 0
+
+
 def test_libm_special_values():
     assert oracle.logf(0.0) == -np.inf
     assert oracle.logf(1.0) == 0.0

@@ -50,7 +50,6 @@ __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y 
 __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
-__device__ __forceinline__ f3 operator/(f3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
 /* Correctly rounded reciprocal 1/x. For |x| in [2^-126, 2^126) it is v_rcp_f32 followed by one FMA Newton step:
  * checked equal to the IEEE quotient 1.0f / x for every binary32 input of that range on gfx950 (all 2^32 bit
  * patterns: tools/rcp_exhaustive.hip, and the device self-test WCPT_SELFTEST_RCP_EXHAUSTIVE run by the GPU tests).
@@ -66,6 +65,15 @@ __device__ __forceinline__ float rcp_exact(float x)
     return 1.0f / x;
 }
 __device__ __forceinline__ f3 rcp3(f3 a) { return mk3(rcp_exact(a.x), rcp_exact(a.y), rcp_exact(a.z)); }
+/* GLSL vector / scalar (normalize, the sphere normal :145, target.xyz / target.w :301, result / samples :312):
+ * v * RN(1/s) with the correctly rounded reciprocal, one reciprocal and three multiplies instead of three
+ * correctly rounded divisions. Vulkan allows 2.5 ULP for GLSL division; this is <= 1.5 ULP, and the oracle
+ * defines vector / scalar the same way (oracle/pt_oracle.c div3s), so the two stay bit-identical. */
+__device__ __forceinline__ f3 operator/(f3 a, float s)
+{
+    const float r = rcp_exact(s);
+    return mk3(a.x * r, a.y * r, a.z * r);
+}
 /* GLSL dot: (x*x' + y*y') + z*z' */
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 /* GLSL cross (4.50 spec §8.5) */
@@ -113,8 +121,8 @@ __device__ __forceinline__ float rand_f(uint32_t& state)
 __device__ __forceinline__ float RandomValueNormalDistribution(uint32_t& seed)
 {
     const float theta = 2.0f * kPI * rand_f(seed);
-    const float rho = sqrtf(-2.0f * wcpt_logf(rand_f(seed)));
-    return rho * wcpt_cosf(theta);
+    const float rho = sqrtf(-2.0f * wcpt_logf_rand(rand_f(seed))); /* == wcpt_logf on rand()'s values */
+    return rho * wcpt_cosf_2pi(theta);                              /* == wcpt_cosf on [0, 2*pi] */
 }
 __device__ __forceinline__ f3 RandomDirection(uint32_t& seed)
 {

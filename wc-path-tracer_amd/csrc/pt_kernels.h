@@ -59,14 +59,18 @@ struct WfBuffers {
     float* wire;       /* gather payload (LaunchArgs::wire) or null                     */
     uint32_t wire_ch;
 };
+/* One pipeline's path state, sized by the pipeline's own path count (its share of the 8x8 tiles), not the frame:
+ * the slot arrays hold only the paths that pipeline can have live at once. The per-pixel sample sums are shared
+ * by the pipelines (WfPipes::result; each pixel belongs to exactly one pipeline). */
 struct WfState {
     void* mem = nullptr;
-    uint32_t capacity = 0;
+    uint32_t capacity = 0;         /* path slots of the arrays in `mem` (set once every allocation succeeded) */
     PathSoA soa[2] = {};
-    float4 *hit = nullptr, *result = nullptr;
+    float4* hit = nullptr;
     uint32_t* ctr = nullptr;
     unsigned long long* diag = nullptr;
-    void* sort_mem = nullptr;
+    void* sort_mem = nullptr;      /* ray-sort scratch, allocated on the first sorted render */
+    uint32_t sort_capacity = 0;
     uint32_t *sort_keys = nullptr, *sort_keys_alt = nullptr, *sort_iota = nullptr, *sort_order = nullptr;
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
@@ -81,6 +85,8 @@ struct WfState {
 constexpr int kWfMaxPipes = 4;
 struct WfPipes {
     WfState pipe[kWfMaxPipes];
+    float4* result = nullptr;            /* by pixel: sum of sample radiance .xyz (all pipelines) */
+    uint64_t result_capacity = 0;        /* pixels */
     hipStream_t aux[kWfMaxPipes] = {};   /* [1..K-1]: created on first use, on the context's device */
     hipEvent_t fork = nullptr;
     hipEvent_t join[kWfMaxPipes] = {};
@@ -98,8 +104,10 @@ constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
 /* Derived triangle records (pt_device.h): triangle k = index positions 3k..3k+2 stored as (a, b - a, c - a);
  * singles: 48 B per triangle; pairs: 80 B per triangle pair (2j, 2j+1). */
 constexpr uint32_t kSingleRecordBytes = 48, kPairRecordBytes = 80;
-hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* singles,
-                                    void* pairs, hipStream_t stream);
+/* vertex_count bounds the vertex indices read (0xFFFFFFFF: unknown); a triangle with an index past it gets a NaN
+ * record, which no ray accepts. */
+hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles,
+                                    uint32_t vertex_count, void* singles, void* pairs, hipStream_t stream);
 /* composite.comp (pt_composite.hip): gamma + PBR Neutral over `pixels` float4 texels into rgba32f or RGBA8 */
 hipError_t launch_composite(const float4* img, uint64_t pixels, void* dst, bool rgba8, int cus, hipStream_t stream);
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream);
@@ -109,6 +117,7 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
 hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes, bool sort_rays, int lds_stack,
                             hipStream_t stream);
 hipError_t wf_reserve(WfState& s, uint32_t paths);
+hipError_t wf_reserve_sort(WfState& s, uint32_t paths);
 void wf_release(WfState& s);
 void wf_release(WfPipes& w);
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n,

@@ -124,10 +124,25 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
 }
 
 /* Derived triangle records (pt_device.h), single and pair formats: one thread per pair. Same subtractions as
- * rayTriangle (:122-123). The second slot of the last pair of an odd count is zero (never inside a leaf's
- * range: leaf_record bounds leaves by the triangle count). */
+ * rayTriangle (:122-123). The second slot of the last pair of an odd count is NaN (never inside a leaf's range:
+ * leaf_record bounds leaves by the triangle count). A vertex index past the vertex buffer gives NaN vertices. */
+__device__ __forceinline__ void tri_fields(const uint32_t* __restrict__ idx, const float* __restrict__ vtx, uint32_t nvert,
+                                           uint64_t k, float f[9])
+{
+    const uint32_t ia = idx[3ull * k + 0], ib = idx[3ull * k + 1], ic = idx[3ull * k + 2];
+    const float qnan = __uint_as_float(0x7fc00000u);
+    const f3 nan3 = mk3(qnan, qnan, qnan);
+    const f3 a = ia < nvert ? ld3(vtx + 3ull * ia) : nan3;
+    const f3 b = ib < nvert ? ld3(vtx + 3ull * ib) : nan3;
+    const f3 c = ic < nvert ? ld3(vtx + 3ull * ic) : nan3;
+    const f3 e1 = b - a, e2 = c - a;
+    f[0] = a.x; f[1] = a.y; f[2] = a.z;
+    f[3] = e1.x; f[4] = e1.y; f[5] = e1.z;
+    f[6] = e2.x; f[7] = e2.y; f[8] = e2.z;
+}
+
 __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restrict__ idx, const float* __restrict__ vtx,
-                                                         uint32_t ntri, float4* __restrict__ singles,
+                                                         uint32_t ntri, uint32_t nvert, float4* __restrict__ singles,
                                                          float4* __restrict__ out)
 {
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
@@ -136,18 +151,15 @@ __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restr
     for (uint32_t h = 0; h < 2; h++) {
         const uint64_t k = 2ull * j + h;
         if (k >= ntri) {
-            for (int c = 0; c < 9; c++) v[h][c] = 0.0f;
+            for (int c = 0; c < 9; c++) v[h][c] = __uint_as_float(0x7fc00000u);
             continue;
         }
-        const uint32_t ia = idx[3ull * k + 0], ib = idx[3ull * k + 1], ic = idx[3ull * k + 2];
-        const f3 a = ld3(vtx + 3ull * ia), b = ld3(vtx + 3ull * ib), c = ld3(vtx + 3ull * ic);
-        const f3 e1 = b - a, e2 = c - a;
-        const float f[9] = {a.x, a.y, a.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z};
-        for (int c2 = 0; c2 < 9; c2++) v[h][c2] = f[c2];
-        singles[3ull * k + 0] = make_float4(a.x, a.y, a.z, e1.x);
-        singles[3ull * k + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+        tri_fields(idx, vtx, nvert, k, v[h]);
+        const f3 e1 = mk3(v[h][3], v[h][4], v[h][5]), e2 = mk3(v[h][6], v[h][7], v[h][8]);
         const f3 n = normalize(cross(e1, e2)); /* :173 */
-        singles[3ull * k + 2] = make_float4(e2.z, n.x, n.y, n.z);
+        singles[3ull * k + 0] = make_float4(v[h][0], v[h][1], v[h][2], v[h][3]);
+        singles[3ull * k + 1] = make_float4(v[h][4], v[h][5], v[h][6], v[h][7]);
+        singles[3ull * k + 2] = make_float4(v[h][8], n.x, n.y, n.z);
     }
     float4* o = out + (uint64_t)kPairRecordFloat4s * j;
     o[0] = make_float4(v[0][0], v[1][0], v[0][1], v[1][1]);
@@ -207,13 +219,13 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
 } // namespace dev
 
 /* ------------------------------------------------------------------------------------------------ */
-hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles, void* singles,
-                                    void* pairs, hipStream_t stream)
+hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles,
+                                    uint32_t vertex_count, void* singles, void* pairs, hipStream_t stream)
 {
     if (triangles == 0) return hipSuccess;
     const uint32_t npairs = (uint32_t)((triangles + 1ull) / 2ull);
     hipLaunchKernelGGL(dev::build_tri_records, dim3((npairs + 255u) / 256u), dim3(256), 0, stream, indices, vertices,
-                       triangles, static_cast<float4*>(singles), static_cast<float4*>(pairs));
+                       triangles, vertex_count, static_cast<float4*>(singles), static_cast<float4*>(pairs));
     return hipGetLastError();
 }
 

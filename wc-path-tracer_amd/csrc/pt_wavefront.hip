@@ -497,11 +497,13 @@ static hipError_t cu_count(WfState& s, int& cus)
 hipError_t wf_reserve(WfState& s, uint32_t paths)
 {
     if (paths <= s.capacity) return hipSuccess;
-    wf_release(s);
+    if (s.mem) (void)hipFree(s.mem);
+    s.mem = nullptr;
+    s.capacity = 0;
     const size_t P = paths;
-    /* two slot-indexed state sets (5 float4 + 2 u32 arrays each), the hit records, the per-pixel sample sums,
-     * then the counters and the diagnostics block */
-    const size_t bytes = P * (2 * (5 * sizeof(float4) + 2 * sizeof(uint32_t)) + 2 * sizeof(float4)) + 256;
+    /* two slot-indexed state sets (5 float4 + 2 u32 arrays each), the hit records by input slot, then the counters
+     * and the diagnostics block */
+    const size_t bytes = P * (2 * (5 * sizeof(float4) + 2 * sizeof(uint32_t)) + sizeof(float4)) + 256;
     char* m = nullptr;
     hipError_t e = hipMalloc(&m, bytes);
     if (e != hipSuccess) return e;
@@ -517,8 +519,7 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
         f += 5 * P;
     }
     s.hit = f;
-    s.result = f + P;
-    uint32_t* u = reinterpret_cast<uint32_t*>(f + 2 * P);
+    uint32_t* u = reinterpret_cast<uint32_t*>(f + P);
     for (int k = 0; k < 2; k++) {
         s.soa[k].pre_prim = u;
         s.soa[k].pix = u + P;
@@ -526,11 +527,22 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     }
     s.ctr = u; /* [0] count q0, [1] count q1, [2] trace head */
     s.diag = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(s.ctr + 4 + 7) & ~uintptr_t(7));
-    s.capacity = paths;
-    /* ray-sort scratch: keys, alternate keys, slot ids, sorted order, radix-sort temporary storage */
+    s.capacity = paths; /* only now: every array above exists */
+    return hipSuccess;
+}
+
+/* Ray-sort scratch (WCPT_OPTION_SORT_RAYS): keys, alternate keys, slot ids, sorted order, radix-sort temporary
+ * storage. Allocated on the first sorted render; capacity is set only once both steps succeeded. */
+hipError_t wf_reserve_sort(WfState& s, uint32_t paths)
+{
+    if (paths <= s.sort_capacity) return hipSuccess;
+    if (s.sort_mem) (void)hipFree(s.sort_mem);
+    s.sort_mem = nullptr;
+    s.sort_capacity = 0;
+    const size_t P = paths;
     size_t temp = 0;
-    e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)paths, 0, 32);
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                      (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)paths, 0, 32);
     if (e != hipSuccess) return e;
     char* q = nullptr;
     e = hipMalloc(&q, 4 * P * sizeof(uint32_t) + temp + 256);
@@ -542,6 +554,20 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
     s.sort_order = s.sort_iota + P;
     s.sort_temp = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(s.sort_order + P) + 255) & ~uintptr_t(255));
     s.sort_temp_bytes = temp;
+    s.sort_capacity = paths;
+    return hipSuccess;
+}
+
+/* Per-pixel sample sums shared by the pipelines (each pixel belongs to one pipeline). */
+static hipError_t wf_reserve_result(WfPipes& w, uint64_t pixels)
+{
+    if (pixels <= w.result_capacity) return hipSuccess;
+    if (w.result) (void)hipFree(w.result);
+    w.result = nullptr;
+    w.result_capacity = 0;
+    hipError_t e = hipMalloc(&w.result, pixels * sizeof(float4));
+    if (e != hipSuccess) return e;
+    w.result_capacity = pixels;
     return hipSuccess;
 }
 
@@ -560,6 +586,7 @@ void wf_release(WfPipes& w)
         if (w.join[j]) (void)hipEventDestroy(w.join[j]);
     }
     if (w.fork) (void)hipEventDestroy(w.fork);
+    if (w.result) (void)hipFree(w.result);
     w = WfPipes{};
 }
 
@@ -647,6 +674,8 @@ static hipError_t wf_dispatch(int mode, bool single, int ldsn, bool query, int& 
 static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b, uint32_t P, int cus,
                              hipStream_t stream)
 {
+    hipError_t r = wf_reserve_sort(s, P);
+    if (r != hipSuccess) return r;
     const uint32_t grid = min((P + 255u) / 256u, (uint32_t)cus * 8u);
     hipLaunchKernelGGL(wf_sort_keys, dim3(grid), dim3(256), 0, stream, b, P, a.draws, s.sort_keys, s.sort_iota);
     hipError_t e = hipGetLastError();
@@ -658,15 +687,16 @@ static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b
 }
 
 /* One pipeline: init + samples*(maxBounce+1) trace/shade iterations over the tiles t with t % npipes == pipe. */
-static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, uint32_t pipe,
-                              uint32_t npipes, bool sort_rays, int ldsn, int cus, uint32_t trace_grid,
+static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, float4* result,
+                              uint32_t pipe, uint32_t npipes, bool sort_rays, int ldsn, int cus, uint32_t trace_grid,
                               uint32_t shade_grid, hipStream_t stream)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
     if (pipe >= tiles) return hipSuccess;
     const uint32_t total = ((tiles - pipe + npipes - 1u) / npipes) * 64u;
-    const uint32_t P = a.W * a.rows;
+    /* live paths of this pipeline <= its pixels: the slot arrays are sized by its share of the tiles, not the frame */
+    const uint32_t P = min(total, a.W * a.rows);
     hipError_t e = wf_reserve(s, P);
     if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
@@ -676,7 +706,7 @@ static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const W
     WfBuffers b;
     b.in = s.soa[0];
     b.out = s.soa[1];
-    b.result = s.result;
+    b.result = result;
     b.hit = s.hit;
     b.order = nullptr;
     b.head = s.ctr + 2;
@@ -754,7 +784,9 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     if (sort_rays || mode == kModeDiag) K = 1; /* one sort scratch and one diagnostics block */
     const uint32_t tiles = tilesX * tilesY;
     if (K > tiles) K = tiles;
-    if (K == 1) return launch_pipe(a, mode, s0, s0, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream);
+    e = wf_reserve_result(w, (uint64_t)a.W * a.rows);
+    if (e != hipSuccess) return e;
+    if (K == 1) return launch_pipe(a, mode, s0, s0, w.result, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream);
 
     /* fork: pipelines 1..K-1 run on their own streams after everything already queued on the context's stream */
     if (!w.fork) {
@@ -779,7 +811,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     }
     hipError_t first = hipSuccess;
     for (uint32_t j = 0; j < K && first == hipSuccess; j++)
-        first = launch_pipe(a, mode, w.pipe[j], s0, j, K, false, ldsn, cus, trace_grid, shade_grid,
+        first = launch_pipe(a, mode, w.pipe[j], s0, w.result, j, K, false, ldsn, cus, trace_grid, shade_grid,
                             j == 0 ? stream : w.aux[j]);
     /* join: the context's stream continues after every pipeline (also after a failed enqueue) */
     for (uint32_t j = 1; j < K; j++) {

@@ -10,6 +10,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -39,11 +40,33 @@ struct Buffer {
     uint64_t bytes = 0;
     uint64_t generation = 0;      /* context-wide counter value of the last alloc / upload / grow */
     std::vector<uint8_t> shadow;  /* host copy of the uploaded contents (buffers <= kShadowMax bytes) */
+    std::vector<uint8_t> known;   /* per kShadowChunk bytes: 1 when `shadow` holds what wcpt_buffer_upload wrote */
 };
 
 /* Small buffers (draw commands, materials, spheres) keep a host copy of what was uploaded, so that the render
  * call can read the draw commands without a device round trip. */
 constexpr uint64_t kShadowMax = 1ull << 20;
+/* Granularity of the host copy's validity map. hipMalloc contents are undefined, so a byte range of the host copy is
+ * trusted only where wcpt_buffer_upload wrote it; any other range is read from the device. */
+constexpr uint64_t kShadowChunk = 32;
+
+/* Mark the chunks of [offset, end) that the upload covers entirely as known (partially covered chunks keep their
+ * state: the host copy is updated byte-exactly either way). */
+void shadow_mark(Buffer& b, uint64_t offset, uint64_t end)
+{
+    if (b.known.empty()) return;
+    const uint64_t c0 = (offset + kShadowChunk - 1) / kShadowChunk, c1 = end / kShadowChunk;
+    for (uint64_t c = c0; c < c1 && c < b.known.size(); c++) b.known[c] = 1;
+}
+
+/* True when the host copy holds every byte of [offset, offset + bytes). */
+bool shadow_known(const Buffer& b, uint64_t offset, uint64_t bytes)
+{
+    if (b.shadow.size() != b.bytes || bytes == 0 || offset + bytes > b.bytes) return false;
+    for (uint64_t c = offset / kShadowChunk; c < (offset + bytes + kShadowChunk - 1) / kShadowChunk; c++)
+        if (c >= b.known.size() || !b.known[c]) return false;
+    return true;
+}
 
 /* Derived triangle records of one draw command (pt_device.h): rebuilt when the draw's vertex/index buffers,
  * their generations or its index count change (or on every render with WCPT_OPTION_TRIANGLE_CACHE = 0). */
@@ -206,8 +229,11 @@ Buffer* buffer_at(wcpt_context* ctx, uint64_t addr, uint64_t& offset)
     return nullptr;
 }
 
-/* Derive (or reuse) the triangle records of every draw command and point a.tri_records at the table. The
- * draw commands are read from the host copy of their buffer when the context owns it, else from the device. */
+/* Derive (or reuse) the triangle records of every draw command and point a.tri_records at the table. The draw
+ * commands are read from the host copy of their buffer when every byte of them was written through
+ * wcpt_buffer_upload and the triangle cache is on; otherwise from the device (a synchronous copy of 32 B per draw),
+ * so that draw commands written by other means (hipMemcpy, the application's own kernels) are honoured with
+ * WCPT_OPTION_TRIANGLE_CACHE = 0. */
 int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t draws, wcpt::LaunchArgs& a)
 {
     const uint32_t n = sd.drawCommandCount;
@@ -217,7 +243,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
     const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
     uint64_t off = 0;
     Buffer* db = buffer_at(ctx, draws, off);
-    if (db && off + dbytes <= db->shadow.size()) {
+    if (ctx->tri_cache && db && shadow_known(*db, off, dbytes)) {
         std::memcpy(dc.data(), db->shadow.data() + off, dbytes);
     } else {
         HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
@@ -232,12 +258,21 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
     for (uint32_t d = 0; d < n; d++) {
         TriRecords& t = ctx->tri[d];
         const uint64_t vb = dc[d].vertexBuffer, ib = dc[d].indexBuffer;
-        uint64_t o = 0;
-        Buffer* bv = buffer_at(ctx, vb, o);
-        Buffer* bi = buffer_at(ctx, ib, o);
+        uint64_t ov = 0, oi = 0, o = 0;
+        Buffer* bv = buffer_at(ctx, vb, ov);
+        Buffer* bi = buffer_at(ctx, ib, oi);
         const uint64_t gv = bv ? bv->generation : kUnknownGeneration;
         const uint64_t gi = bi ? bi->generation : kUnknownGeneration;
         const uint32_t ntri = dc[d].indexCount / 3u;
+        /* The records are built from indices [0, indexCount) of the draw: an index buffer known to the context must
+         * hold them (the reference's kernel never reads indexCount, but the record build does). Vertex indices are
+         * checked against the vertex buffer's size on the device (an out-of-range index gives a triangle that is
+         * never hit, instead of a read past the buffer). */
+        if (bi && (uint64_t)ntri * 12ull > bi->bytes - oi)
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT,
+                             "draw command %u: indexCount %u exceeds its index buffer (%llu bytes from offset %llu)", d,
+                             dc[d].indexCount, (unsigned long long)(bi->bytes - oi), (unsigned long long)oi);
+        const uint32_t nvert = bv ? (uint32_t)std::min<uint64_t>((bv->bytes - ov) / 12ull, 0xFFFFFFFFull) : 0xFFFFFFFFu;
         const bool reuse = ctx->tri_cache && t.valid && t.vb == vb && t.ib == ib && t.ntri == ntri && t.gen_vb == gv &&
                            t.gen_ib == gi && gv != kUnknownGeneration && gi != kUnknownGeneration;
         if (!reuse) {
@@ -255,7 +290,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
                 return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "draw command %u: null vertex/index buffer", d);
             t.pair_offset = singles;
             HIP_TRY(ctx, wcpt::launch_build_tri_records(reinterpret_cast<const uint32_t*>(ib),
-                                                        reinterpret_cast<const float*>(vb), ntri, t.mem,
+                                                        reinterpret_cast<const float*>(vb), ntri, nvert, t.mem,
                                                         static_cast<char*>(t.mem) + singles, ctx->stream),
                     "build_tri_records");
             t.vb = vb;
@@ -541,6 +576,7 @@ int wcpt_buffer_alloc(wcpt_context* ctx, uint64_t bytes, wcpt_buffer* out)
     HIP_TRY(ctx, skewed_alloc(b, bytes), "hipMalloc(buffer)");
     b.generation = ++ctx->generation;
     if (bytes <= kShadowMax) b.shadow.assign(bytes, 0); /* hipMalloc contents are undefined; see upload */
+    if (bytes <= kShadowMax) b.known.assign((bytes + kShadowChunk - 1) / kShadowChunk, 0);
     const uint64_t h = ctx->next_handle++;
     ctx->buffers[h] = b;
     *out = h;
@@ -554,10 +590,14 @@ int wcpt_buffer_upload(wcpt_context* ctx, wcpt_buffer buf, const void* src, uint
     Buffer* b = find_buffer(ctx, buf);
     if (!b) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle %llu", (unsigned long long)buf);
     if (bytes && !src) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null upload source");
-    if (offset + bytes > b->bytes) {
+    uint64_t end = 0;
+    if (__builtin_add_overflow(offset, bytes, &end) || end > (1ull << 48))
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "upload range offset %llu + %llu bytes overflows",
+                         (unsigned long long)offset, (unsigned long long)bytes);
+    if (end > b->bytes) {
         /* grow, keeping the old contents (BufferManager.jai:53-54 reallocates on growth) */
         Buffer nb;
-        HIP_TRY(ctx, skewed_alloc(nb, offset + bytes), "hipMalloc(buffer grow)");
+        HIP_TRY(ctx, skewed_alloc(nb, end), "hipMalloc(buffer grow)");
         if (b->ptr && b->bytes) {
             hipError_t e = hipMemcpyAsync(nb.ptr, b->ptr, b->bytes, hipMemcpyDeviceToDevice, ctx->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -568,15 +608,24 @@ int wcpt_buffer_upload(wcpt_context* ctx, wcpt_buffer buf, const void* src, uint
         }
         if (b->raw) (void)hipFree(b->raw);
         nb.shadow = std::move(b->shadow);
+        nb.known = std::move(b->known);
         *b = std::move(nb);
-        if (b->bytes <= kShadowMax) b->shadow.resize(b->bytes, 0);
-        else b->shadow.clear();
+        if (b->bytes <= kShadowMax) {
+            b->shadow.resize(b->bytes, 0);
+            b->known.resize((b->bytes + kShadowChunk - 1) / kShadowChunk, 0); /* the grown tail is undefined */
+        } else {
+            b->shadow.clear();
+            b->known.clear();
+        }
     }
     if (bytes) {
         HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(b->ptr) + offset, src, bytes, hipMemcpyHostToDevice, ctx->stream),
                 "hipMemcpyAsync(upload)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(upload)"); /* blocking, like :98-112 */
-        if (b->shadow.size() == b->bytes && b->bytes) std::memcpy(b->shadow.data() + offset, src, bytes);
+        if (b->shadow.size() == b->bytes && b->bytes) {
+            std::memcpy(b->shadow.data() + offset, src, bytes);
+            shadow_mark(*b, offset, end);
+        }
     }
     b->generation = ++ctx->generation;
     return WCPT_SUCCESS;
@@ -588,7 +637,8 @@ int wcpt_buffer_download(wcpt_context* ctx, wcpt_buffer buf, void* dst, uint64_t
     if (rc) return rc;
     Buffer* b = find_buffer(ctx, buf);
     if (!b) return set_error(ctx, WCPT_ERROR_INVALID_HANDLE, "unknown buffer handle %llu", (unsigned long long)buf);
-    if (offset + bytes > b->bytes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "download out of range");
+    if (bytes > b->bytes || offset > b->bytes - bytes)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "download out of range");
     if (bytes && !dst) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null download destination");
     if (bytes) {
         HIP_TRY(ctx, hipMemcpyAsync(dst, static_cast<char*>(b->ptr) + offset, bytes, hipMemcpyDeviceToHost, ctx->stream),
