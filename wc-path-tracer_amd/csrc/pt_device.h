@@ -323,11 +323,44 @@ __device__ __forceinline__ uint32_t leaf_record(uint32_t first, uint32_t count, 
     return (k * 3u == first && (uint64_t)k + (count + 2u) / 3u <= ntri) ? k : kNoRecord;
 }
 
+/* Megakernel phase timers (tools only: a library built with -DWCPT_MK_TIMERS=1, tools/mk_phases.py). Each wave
+ * attributes the s_memtime ticks since its previous mark to the phase that just ended: 0 primary ray, 1 sphere
+ * loop, 2 BVH interior steps + pops, 3 leaf triangle tests, 4 hit resolution, 5 shading, 6 accumulation/store.
+ * Ticks include the time other waves of the SIMD issue in between: read the shares, not absolute costs. */
+#ifndef WCPT_MK_TIMERS
+#define WCPT_MK_TIMERS 0
+#endif
+constexpr int kPhaseTimers = 8;
+
 /* Per-lane work counters; reduced per wave and added to global u64 counters. */
 struct Counters {
     uint32_t pixels, segments, sphere_tests, node_pops, interior_visits, triangle_tests, hits, draw_fetches;
     uint32_t wave_int, lane_int, wave_tri, lane_tri, wave_seg, lane_seg; /* SIMD-efficiency diagnostics */
+#if WCPT_MK_TIMERS
+    uint64_t tim[kPhaseTimers], tprev;
+#endif
 };
+
+__device__ __forceinline__ void phase_start(Counters& c)
+{
+#if WCPT_MK_TIMERS
+    for (int k = 0; k < kPhaseTimers; k++) c.tim[k] = 0;
+    c.tprev = __builtin_amdgcn_s_memtime();
+#else
+    (void)c;
+#endif
+}
+__device__ __forceinline__ void phase_mark(Counters& c, int k)
+{
+#if WCPT_MK_TIMERS
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    c.tim[k] += t - c.tprev;
+    c.tprev = t;
+#else
+    (void)c;
+    (void)k;
+#endif
+}
 
 /* Diagnostic step counting (COUNT kernels only): every executing lane adds a lane-step, the lowest active
  * lane adds the wave-step. */
@@ -498,6 +531,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
             prim = kSpherePrim | i;
         }
     }
+    phase_mark(cnt, 1);
 
     for (uint32_t i = 0; i < sd.drawCommandCount; i++) {
         const gnode_ptr bvh = as_nodes(draws[i].bvhBuffer);
@@ -560,6 +594,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                         }
                     }
                 }
+                phase_mark(cnt, 3);
             } else {
                 /* interior (:179-199): fetch both children (64 contiguous bytes), test both boxes */
                 const NodeV L = load_node(bvh, curLeft);
@@ -589,6 +624,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                     const NodeV& N = leftFirst ? L : R;
                     curLeft = N.b.z;
                     curCount = N.b.w;
+                    phase_mark(cnt, 2);
                     continue;
                 }
             }
@@ -605,13 +641,16 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 found = true;
                 break;
             }
+            phase_mark(cnt, 2);
             if (!found) break;
         }
         if (rt != rt_before) primDraw = i;
     }
 
     if (COUNT && prim != kNoPrim) cnt.hits++;
-    return resolve_hit(ray, rt, prim, primDraw, spheres, draws, tri_records);
+    const Hit hit = resolve_hit(ray, rt, prim, primDraw, spheres, draws, tri_records);
+    phase_mark(cnt, 4);
+    return hit;
 }
 
 /* pathTracer.comp:213-234 */
@@ -721,7 +760,9 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
     f3 L;
     for (;;) {
         const Hit h = intersect<COUNT, DIAG, PAIRS>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
-        if (path_shade(ps, h, rng, sd, mats, L)) return L;
+        const bool done = path_shade(ps, h, rng, sd, mats, L);
+        phase_mark(cnt, 5);
+        if (done) return L;
     }
 }
 

@@ -53,6 +53,12 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
     const f3 dir = primary_direction(sd, x, y, W, H);
     const uint32_t pixel_index = x + y * W + sd.renderedFramesCount * 719393u; /* :304 */
     uint32_t seed = pcg_hash(pixel_index);
+    /* The accumulation read (:314) is issued before the trace, so its HBM latency hides behind the segments
+     * instead of stalling the wave at its end (the image is the one buffer that does not live in L2). */
+    float4* px = image + (size_t)ly * W + lx;
+    float4 old = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!COUNT && sd.renderedFramesCount != 0) old = *px;
+    phase_mark(cnt, 0);
     f3 result = mk3(0.0f, 0.0f, 0.0f);
     const f3 origin = mk3(sd.position[0], sd.position[1], sd.position[2]);
     for (uint32_t s = 0; s < sd.samples; s++) { /* :309-310, all samples share the primary ray */
@@ -64,12 +70,11 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
     }
     result = result / (float)sd.samples; /* :312 */
     if (!COUNT) {
-        float4* px = image + (size_t)ly * W + lx;
         f3 acc;
         if (sd.renderedFramesCount == 0) { /* :318 — the loaded value would be discarded */
             acc = result;
         } else {
-            const float4 o = *px;                                             /* :314 */
+            const float4 o = old;                                             /* :314 */
             const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u); /* :316 */
             const float iw = 1.0f - weight;
             acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight, o.z * iw + result.z * weight);
@@ -77,6 +82,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
         store_pixel(image, wire, wire_ch, (size_t)ly * W + lx, acc); /* :323 */
     }
     if (COUNT) cnt.pixels++;
+    phase_mark(cnt, 6);
 }
 
 /* Stack kinds: 0 = private (scratch) stack of kPrivateStack entries; 1 = LDS stack of kLdsStack entries per
@@ -101,6 +107,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
     const uint32_t lx = tx * kTileW + (threadIdx.x % kTileW);
     const uint32_t ly = ty * kTileH + (threadIdx.x / kTileW);
     Counters cnt = {};
+    phase_start(cnt);
     bool overflow = false;
     if (lx < W && ly < rows) {
         if constexpr (SK == 0) {
@@ -121,6 +128,10 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
     }
     if (overflow) atomicOr(status, 1u);
     flush_counters<COUNT>(cnt, counters);
+#if WCPT_MK_TIMERS
+    if (!COUNT && (threadIdx.x & 63u) == 0u)
+        for (int k = 0; k < kPhaseTimers; k++) atomicAdd(&counters[k], (unsigned long long)cnt.tim[k]);
+#endif
 }
 
 /* Derived triangle records (pt_device.h), single and pair formats: one thread per pair. Same subtractions as
@@ -204,6 +215,21 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
         break;
     }
     case 9: out[i] = __float_as_uint(rcp_exact(__uint_as_float(a))); break;
+    case 10:   /* as 8, over every normal binary32 input (v_cmp_class range test) */
+    case 11: { /* as 8, over every input (no range test) */
+        uint32_t bad = 0;
+        for (uint32_t k = 0; k < 65536u; k++) {
+            const float x = __uint_as_float((a << 16) | k);
+            if (fn == 10 && !__builtin_isnormal(x)) continue;
+            const float y = __builtin_amdgcn_rcpf(x);
+            const float e = __builtin_fmaf(-x, y, 1.0f);
+            const float r = __builtin_fmaf(e, y, y);
+            const float q = 1.0f / x;
+            bad += (__float_as_uint(r) != __float_as_uint(q) && !(r != r && q != q)) ? 1u : 0u;
+        }
+        out[i] = bad;
+        break;
+    }
     case 7: { /* RandomDirection: 3 words per input */
         uint32_t s = a;
         const f3 d = RandomDirection(s);

@@ -397,6 +397,12 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     }
     rc = prepare_tri_records(ctx, *scene, draws, a);
     if (rc) return rc;
+#if WCPT_MK_TIMERS
+    /* tools-only build: the render's megakernel adds its phase timers to the counters (wcpt_read_diagnostics) */
+    if (mode == wcpt::kModeRender && ctx->kernel == WCPT_KERNEL_MEGAKERNEL)
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream),
+                "hipMemsetAsync(timers)");
+#endif
     hipError_t e = hipSuccess;
     switch (ctx->kernel) {
     case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->mk, ctx->stream); break;
@@ -872,6 +878,14 @@ int wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n)
     if (rc) return rc;
     if (!out || n > 8) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_read_diagnostics: bad output");
     memset(out, 0, sizeof(uint64_t) * n);
+#if WCPT_MK_TIMERS
+    if (ctx->kernel == WCPT_KERNEL_MEGAKERNEL && n) { /* megakernel phase timers of the last render */
+        HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_counters, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream),
+                "hipMemcpyAsync(timers)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+        return WCPT_SUCCESS;
+    }
+#endif
     if (!ctx->wf.pipe[0].diag || n == 0) return WCPT_SUCCESS;
     HIP_TRY(ctx, hipMemcpyAsync(out, ctx->wf.pipe[0].diag, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream),
             "hipMemcpyAsync(diag)");
@@ -913,7 +927,7 @@ int wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const ui
     int rc = bind(ctx);
     if (rc) return rc;
     if (!in || !out || (fn == 6 && !in2)) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
-    if (fn < 0 || fn > 9) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
+    if (fn < 0 || fn > 11) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
     const uint64_t outw = (fn == 1) ? 4ull * n : (fn == 7 ? 3ull * n : (uint64_t)n);
     rc = ensure_scratch(ctx, (2ull * n + outw) * 4ull + 16);
     if (rc) return rc;
