@@ -124,6 +124,40 @@ def test_device_fast_reciprocal_exhaustive(gpu_ctx):
     assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))
 
 
+def test_device_reciprocal_result_check_exhaustive(gpu_ctx):
+    """The kernels validate the fast reciprocal on its result class (pt_device.h rcp_exact / rcp2_exact): over
+    ALL 2^32 inputs, in the scalar form and in both halves of the packed pair form, the result is IEEE 1/x
+    (fn 12), and the general division runs exactly for the inputs outside [2^-126, 2^126] (fn 13): zeros and
+    denormals (exponent field 0), |x| in (2^126, 2^128), infinities and NaNs (exponent fields 253..255 minus the
+    two patterns +-2^126, whose quotient +-2^-126 is normal): 2 * 4 * 2^23 - 2 = 2^26 - 2 bit patterns."""
+    hi = np.arange(65536, dtype=np.uint32)
+    bad = gpu_ctx.selftest(12, hi)
+    assert int(bad.sum()) == 0, f"reciprocal differs from IEEE on {int(bad.sum())} inputs"
+    slow = int(gpu_ctx.selftest(13, hi).astype(np.uint64).sum())
+    assert slow == 2 ** 26 - 2
+
+
+def test_device_acceptance_forms_agree(gpu_ctx):
+    """accept_tri (four compares, the reference's :132 minus the implied u <= 1) and accept_tri_w (minimum3 form
+    used by the pair test) decide identically on special and random (u, v)."""
+    special = np.array([0.0, -0.0, 1.0, -1.0, 0.5, 1e-45, -1e-45, 1.0000001, 0.99999994, 0.49999997, 0.50000006,
+                        np.inf, -np.inf, np.nan, -np.nan, 3.4028235e38, -3.4028235e38, 2.0, 1e-30, -1e-30],
+                       np.float32)
+    uu, vv = np.meshgrid(special, special)
+    rng = np.random.default_rng(14)
+    ru = rng.uniform(-0.2, 1.2, 200000).astype(np.float32)
+    rv = rng.uniform(-0.2, 1.2, 200000).astype(np.float32)
+    # near the u + v = 1 edge: v = 1 - u and its neighbours
+    eu = rng.uniform(0.0, 1.0, 100000).astype(np.float32)
+    ev = (np.float32(1.0) - eu).view(np.uint32) + rng.integers(-2, 3, 100000).astype(np.int64).astype(np.uint32)
+    u = np.concatenate([uu.ravel(), ru, eu])
+    v = np.concatenate([vv.ravel(), rv, ev.view(np.float32)])
+    out = gpu_ctx.selftest(14, u.view(np.uint32), v.view(np.uint32))
+    assert np.array_equal(out & 1, out >> 1), f"{int(((out & 1) != (out >> 1)).sum())} disagreements"
+    assert int((out & 1).sum()) > 1000  # both accepting and rejecting cases are exercised
+    assert int((out & 1).sum()) < u.size
+
+
 def test_device_random_direction(gpu_ctx):
     x = np.arange(1000, dtype=np.uint32) * 2654435761
     out = gpu_ctx.selftest(7, x).view(np.float32).reshape(-1, 3)

@@ -50,19 +50,62 @@ __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y 
 __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
-/* Correctly rounded reciprocal 1/x. For |x| in [2^-126, 2^126) it is v_rcp_f32 followed by one FMA Newton step:
- * checked equal to the IEEE quotient 1.0f / x for every binary32 input of that range on gfx950 (all 2^32 bit
- * patterns: tools/rcp_exhaustive.hip, and the device self-test WCPT_SELFTEST_RCP_EXHAUSTIVE run by the GPU tests).
- * 3 VALU instead of the 11 of hipcc's general division sequence; other inputs take that sequence. */
+/* Correctly rounded reciprocal 1/x: v_rcp_f32 followed by one FMA Newton step, with the general division for the
+ * inputs where that fast sequence is not the IEEE quotient. 3 VALU + 1 check instead of the 11 of hipcc's
+ * division sequence.
+ *
+ * The fast sequence equals 1.0f / x for every |x| in [2^-126, 2^126) (all 2^32 bit patterns checked on gfx950:
+ * tools/rcp_exhaustive.hip and selftest fn 8/10). Outside that range it returns zero (|x| >= 2^126: the denormal
+ * quotient is flushed) or NaN (x zero, denormal, infinite or NaN), never a normal number. So the fast result is
+ * validated on its own class (one v_cmp_class): a normal result is the IEEE quotient, anything else takes the
+ * general division. Checked over all 2^32 inputs: selftest fn 12 (0 mismatches), which also runs the packed pair
+ * form rcp2_exact. WCPT_RCP_RANGE=1 selects the older input-range test (two compares). */
+#ifndef WCPT_RCP_RANGE
+#define WCPT_RCP_RANGE 0
+#endif
+__device__ __forceinline__ float rcp_fast_raw(float x)
+{
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y, 1.0f);
+    return __builtin_fmaf(e, y, y);
+}
+__device__ __forceinline__ bool rcp_fast_ok(float r) { return __builtin_isnormal(r); }
 __device__ __forceinline__ float rcp_exact(float x)
 {
+#if WCPT_RCP_RANGE
     const float a = fabsf(x);
-    if (__builtin_expect(a >= 0x1p-126f && a < 0x1p126f, 1)) {
-        const float y = __builtin_amdgcn_rcpf(x);
-        const float e = __builtin_fmaf(-x, y, 1.0f);
-        return __builtin_fmaf(e, y, y);
-    }
+    if (__builtin_expect(a >= 0x1p-126f && a < 0x1p126f, 1)) return rcp_fast_raw(x);
     return 1.0f / x;
+#else
+    const float r = rcp_fast_raw(x);
+    if (__builtin_expect(rcp_fast_ok(r), 1)) return r;
+    return 1.0f / x;
+#endif
+}
+typedef float v2f __attribute__((ext_vector_type(2)));
+/* rcp_exact of both halves: two v_rcp_f32, the Newton step as two packed FMAs (v_pk_fma_f32: two independent
+ * binary32 fused multiply-adds, the same operations as the scalar step) and one branch for both fallbacks. */
+__device__ __forceinline__ v2f rcp2_exact(v2f x)
+{
+#if WCPT_RCP_RANGE
+    v2f r;
+    r.x = rcp_exact(x.x);
+    r.y = rcp_exact(x.y);
+    return r;
+#else
+    v2f y;
+    y.x = __builtin_amdgcn_rcpf(x.x);
+    y.y = __builtin_amdgcn_rcpf(x.y);
+    const v2f one = {1.0f, 1.0f};
+    const v2f e = __builtin_elementwise_fma(-x, y, one);
+    v2f r = __builtin_elementwise_fma(e, y, y);
+    const bool okx = rcp_fast_ok(r.x), oky = rcp_fast_ok(r.y);
+    if (__builtin_expect(!(okx && oky), 0)) {
+        if (!okx) r.x = 1.0f / x.x;
+        if (!oky) r.y = 1.0f / x.y;
+    }
+    return r;
+#endif
 }
 __device__ __forceinline__ f3 rcp3(f3 a) { return mk3(rcp_exact(a.x), rcp_exact(a.y), rcp_exact(a.z)); }
 /* GLSL vector / scalar (normalize, the sphere normal :145, target.xyz / target.w :301, result / samples :312):
@@ -210,6 +253,26 @@ __device__ __forceinline__ bool accept_tri(float t, float u, float v, float uv)
     return t > 0.0f && u >= 0.0f && v >= 0.0f && uv <= 1.0f;
 }
 
+/* The same decision with one compare for u, v and u + v: t > 0 && minimum3(u, v, 1 - (u + v)) >= 0, where minimum3
+ * is v_minimum3_f32 (IEEE 754-2019 minimum: NaN-propagating, -0 < +0). Equivalence: a NaN u or v makes u + v and
+ * 1 - (u + v) NaN, so the minimum is NaN and the test fails, as `u >= 0` / `v >= 0` does; u = +inf with v = -inf
+ * fails both ways (v < 0, and the NaN sum). For non-NaN values minimum3 >= 0 is u >= 0 && v >= 0 && w >= 0 (-0 counts
+ * as >= 0 in both), and w = RN(1 - uv) >= 0 exactly when uv <= 1: uv <= 1 makes 1 - uv >= 0, whose rounding stays
+ * >= 0; uv > 1 means uv >= 1 + 2^-23, so 1 - uv <= -2^-23 rounds to a negative number; uv = -inf gives +inf and
+ * passes as `uv <= 1` does. The device self-test fn 14 compares both forms on special and random operands. The
+ * pair test forms w for both triangles with one packed subtraction: 4.5 VALU per triangle instead of 5. */
+#ifndef WCPT_ACCEPT_MIN3
+#define WCPT_ACCEPT_MIN3 1
+#endif
+__device__ __forceinline__ float minimum3(float a, float b, float c)
+{
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ bool accept_tri_w(float t, float u, float v, float w)
+{
+    return t > 0.0f && minimum3(u, v, w) >= 0.0f;
+}
+
 /* pathTracer.comp:121-133 with the two edges given: e1 = b - a, e2 = c - a (:122-123); returns t or -1 */
 __device__ __forceinline__ float rayTriangleE(const Ray& r, f3 a, f3 edgeAB, f3 edgeAC)
 {
@@ -256,12 +319,29 @@ __device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
     e.e2 = mk3(r1.z, r1.w, r2.x);
     return e;
 }
-typedef float v2f __attribute__((ext_vector_type(2)));
 constexpr uint32_t kPairRecordFloat4s = 5;
 struct TriPair { v2f ax, ay, az, e1x, e1y, e1z, e2x, e2y, e2z; };
 __device__ __forceinline__ TriPair load_pair(gtri_ptr t, uint32_t j)
 {
     const gtri_ptr q = t + (uint64_t)kPairRecordFloat4s * j;
+    const v4f r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    TriPair p;
+    p.ax = r0.xy;  p.ay = r0.zw;
+    p.az = r1.xy;  p.e1x = r1.zw;
+    p.e1y = r2.xy; p.e1z = r2.zw;
+    p.e2x = r3.xy; p.e2y = r3.zw;
+    p.e2z = r4.xy;
+    return p;
+}
+/* The pair record at byte offset `off` from the record base (pair j at off = 80 j). */
+constexpr uint32_t kPairRecordBytes = 16u * kPairRecordFloat4s;
+constexpr uint32_t kNoTag = 0xFFFFFFFFu;
+#ifndef WCPT_PAIR_OFFSET_LOOP
+#define WCPT_PAIR_OFFSET_LOOP 1
+#endif
+__device__ __forceinline__ TriPair load_pair_at(const WCPT_GLOBAL char* base, uint32_t off)
+{
+    const gtri_ptr q = reinterpret_cast<gtri_ptr>(base + off);
     const v4f r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
     TriPair p;
     p.ax = r0.xy;  p.ay = r0.zw;
@@ -285,9 +365,7 @@ __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& 
     const v2f py = dz * p.e2x - p.e2z * dx;
     const v2f pz = dx * p.e2y - p.e2x * dy;
     const v2f det = (p.e1x * px + p.e1y * py) + p.e1z * pz;
-    v2f inv;
-    inv.x = rcp_exact(det.x);
-    inv.y = rcp_exact(det.y);
+    const v2f inv = rcp2_exact(det);
     /* crossROAE1 = cross(oa, e1) */
     const v2f qx = oay * p.e1z - p.e1y * oaz;
     const v2f qy = oaz * p.e1x - p.e1z * oax;
@@ -298,8 +376,14 @@ __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& 
     const v2f uv = u + v;
     PairHit h;
     h.t = t;
+#if WCPT_ACCEPT_MIN3
+    const v2f w = bc2(1.0f) - uv;
+    h.hit0 = accept_tri_w(t.x, u.x, v.x, w.x);
+    h.hit1 = accept_tri_w(t.y, u.y, v.y, w.y);
+#else
     h.hit0 = accept_tri(t.x, u.x, v.x, uv.x);
     h.hit1 = accept_tri(t.y, u.y, v.y, uv.y);
+#endif
     return h;
 }
 __device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
@@ -566,6 +650,26 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                         if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
                         k++;
                     }
+#if WCPT_PAIR_OFFSET_LOOP
+                    /* whole pairs: one 32-bit byte-offset induction variable from the draw's (uniform) record base
+                     * (global_load with an SGPR base), and the winner recorded as a tag -- the pair's offset for its
+                     * first triangle, offset + 1 for its second -- decoded into the index position once per leaf */
+                    {
+                        const uint32_t kfull = kend & ~1u;
+                        const WCPT_GLOBAL char* pbase = reinterpret_cast<const WCPT_GLOBAL char*>(tris);
+                        const uint32_t offEnd = (kfull >> 1) * kPairRecordBytes;
+                        uint32_t off = (k >> 1) * kPairRecordBytes, tag = kNoTag;
+                        for (; off < offEnd; off += kPairRecordBytes) {
+                            const PairHit ph = rayTrianglePair(ray, load_pair_at(pbase, off));
+                            count_tri<COUNT, DIAG>(cnt);
+                            if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
+                            count_tri<COUNT, DIAG>(cnt);
+                            if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+                        }
+                        if (tag != kNoTag) prim = 3u * (2u * (tag / kPairRecordBytes) + (tag & 1u));
+                        if (k < kfull) k = kfull;
+                    }
+#else
                     for (const uint32_t kfull = kend & ~1u; k < kfull; k += 2) {
                         const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
                         count_tri<COUNT, DIAG>(cnt);
@@ -573,6 +677,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                         count_tri<COUNT, DIAG>(cnt);
                         if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * (k + 1u); }
                     }
+#endif
                     if (k < kend) {
                         const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
                         count_tri<COUNT, DIAG>(cnt);

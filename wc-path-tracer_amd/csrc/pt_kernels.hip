@@ -230,6 +230,38 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
         out[i] = bad;
         break;
     }
+    case 12: { /* the kernels' reciprocals vs the IEEE quotient over the 2^16 inputs x = (a << 16) | k: rcp_exact(x), and
+                  rcp2_exact on the pair (x, ~x) (every bit pattern in both halves); mismatches, NaN == NaN */
+        uint32_t bad = 0;
+        for (uint32_t k = 0; k < 65536u; k++) {
+            const uint32_t bits = (a << 16) | k;
+            const float x = __uint_as_float(bits), x2 = __uint_as_float(~bits);
+            const float r = rcp_exact(x);
+            v2f xx;
+            xx.x = x;
+            xx.y = x2;
+            const v2f rr = rcp2_exact(xx);
+            const float q = 1.0f / x, q2 = 1.0f / x2;
+            bad += (__float_as_uint(r) != __float_as_uint(q) && !(r != r && q != q)) ? 1u : 0u;
+            bad += (__float_as_uint(rr.x) != __float_as_uint(q) && !(rr.x != rr.x && q != q)) ? 1u : 0u;
+            bad += (__float_as_uint(rr.y) != __float_as_uint(q2) && !(rr.y != rr.y && q2 != q2)) ? 1u : 0u;
+        }
+        out[i] = bad;
+        break;
+    }
+    case 13: { /* how many of the 2^16 inputs (a << 16) | k fail the fast result's class check (general division) */
+        uint32_t slow = 0;
+        for (uint32_t k = 0; k < 65536u; k++)
+            slow += rcp_fast_ok(rcp_fast_raw(__uint_as_float((a << 16) | k))) ? 0u : 1u;
+        out[i] = slow;
+        break;
+    }
+    case 14: { /* acceptance tests on (u, v) = (in, in2) with t = 1: bit 0 = accept_tri, bit 1 = accept_tri_w */
+        const float u = __uint_as_float(a), v = __uint_as_float(in2[i]);
+        const float uv = u + v;
+        out[i] = (accept_tri(1.0f, u, v, uv) ? 1u : 0u) | (accept_tri_w(1.0f, u, v, 1.0f - uv) ? 2u : 0u);
+        break;
+    }
     case 7: { /* RandomDirection: 3 words per input */
         uint32_t s = a;
         const f3 d = RandomDirection(s);

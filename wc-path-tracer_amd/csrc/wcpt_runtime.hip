@@ -84,6 +84,9 @@ struct TriRecords {
  * estimated as triangles / leaves with leaves = (nodes + 1) / 2 from the BVH buffer's size. Measured: the
  * Cornell box (17 per leaf) gains, the atrium (~2 per leaf) loses. */
 constexpr double kPairMinTrianglesPerLeaf = 4.0;
+/* Largest triangle count of a draw whose pair records are used: 40 B per triangle must stay addressable with 32-bit
+ * byte offsets (2^26 triangles = 2.5 GiB of pair records); larger draws use single records. */
+constexpr uint64_t kPairMaxTriangles = 1ull << 26;
 
 hipError_t skewed_alloc(Buffer& b, uint64_t bytes)
 {
@@ -254,7 +257,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
     constexpr uint64_t W = 4; /* table words per draw (pt_device.h kTriTableWords) */
     bool table_dirty = ctx->tri_table.size() < W * n;
     if (table_dirty) ctx->tri_table.resize(W * n, 0);
-    uint64_t tris_all = 0, leaves_all = 0;
+    uint64_t tris_all = 0, leaves_all = 0, tris_max = 0;
     for (uint32_t d = 0; d < n; d++) {
         TriRecords& t = ctx->tri[d];
         const uint64_t vb = dc[d].vertexBuffer, ib = dc[d].indexBuffer;
@@ -314,6 +317,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
             }
         }
         tris_all += ntri;
+        tris_max = std::max<uint64_t>(tris_max, ntri);
         leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
     }
     if (ctx->tri_table_cap < n) {
@@ -333,8 +337,10 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(triangle record table)");
     }
     a.tri_records = ctx->d_tri_table;
-    a.pair_records = ctx->pair_records == 1 ||
-                     (ctx->pair_records < 0 && leaves_all > 0 && (double)tris_all >= kPairMinTrianglesPerLeaf * leaves_all);
+    /* pair leaves address a draw's pair records with 32-bit byte offsets (pt_device.h load_pair_at) */
+    a.pair_records = tris_max <= kPairMaxTriangles &&
+                     (ctx->pair_records == 1 ||
+                      (ctx->pair_records < 0 && leaves_all > 0 && (double)tris_all >= kPairMinTrianglesPerLeaf * leaves_all));
     return WCPT_SUCCESS;
 }
 
@@ -926,8 +932,8 @@ int wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const ui
 {
     int rc = bind(ctx);
     if (rc) return rc;
-    if (!in || !out || (fn == 6 && !in2)) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
-    if (fn < 0 || fn > 11) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
+    if (!in || !out || ((fn == 6 || fn == 14) && !in2)) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
+    if (fn < 0 || fn > 14) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
     const uint64_t outw = (fn == 1) ? 4ull * n : (fn == 7 ? 3ull * n : (uint64_t)n);
     rc = ensure_scratch(ctx, (2ull * n + outw) * 4ull + 16);
     if (rc) return rc;
