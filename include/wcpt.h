@@ -302,12 +302,13 @@ void     wcpt_string_free(char* text);
 
 /* ---- self-test entry points (used by the parity tests; GPU) ---------------------------------------- */
 /* Evaluates device functions on n inputs: fn 0 = pcg_hash, 1 = rand stream (4 per input),
- * 2 = log, 3 = cos, 4 = exp, 5 = sqrt, 6 = divide(in, in2), 7 = RandomDirection (3 per input),
+ * 2 = log, 3 = cos, 4 = exp, 5 = sqrt (the kernels' sqrt_exact), 6 = divide(in, in2), 7 = RandomDirection (3 per input),
  * 8 = exhaustive check of the fast reciprocal (out[i] = mismatches vs IEEE 1/x over the bit patterns
  * (in[i] << 16) | k, k < 2^16), 9 = the reciprocal used by the kernels, 10/11 = as 8 over every normal /
  * every input, 12 = as 8 for the kernels' reciprocals (rcp_exact, and its packed pair form on (x, ~x)),
  * 13 = how many inputs of the block fail the fast result's class check (take the general division),
- * 14 = the two triangle acceptance forms on (u, v) = (in, in2) with t = 1 (bit 0 compares, bit 1 minimum3). Host arrays of 32-bit words. */
+ * 14 = the two triangle acceptance forms on (u, v) = (in, in2) with t = 1 (bit 0 compares, bit 1 minimum3),
+ * 15 = as 8 for the kernels' square root (sqrt_exact) against the correctly rounded sqrtf. Host arrays of 32-bit words. */
 int      wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const uint32_t* in2,
                               uint32_t* out, uint32_t n);
 

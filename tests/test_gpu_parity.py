@@ -137,6 +137,14 @@ def test_device_reciprocal_result_check_exhaustive(gpu_ctx):
     assert slow == 2 ** 26 - 2
 
 
+def test_device_sqrt_exhaustive(gpu_ctx):
+    """The kernels' square root (pt_device.h sqrt_exact: the 9-VALU correction core for x >= 2^-96, hipcc's full
+    sequence elsewhere) equals hipcc's correctly rounded sqrtf on ALL 2^32 inputs (fn 15); test_device_sqrt_div_ieee
+    checks it against numpy on random magnitudes."""
+    bad = gpu_ctx.selftest(15, np.arange(65536, dtype=np.uint32))
+    assert int(bad.sum()) == 0, f"sqrt differs on {int(bad.sum())} inputs, first high halves {np.nonzero(bad)[0][:8]}"
+
+
 def test_device_acceptance_forms_agree(gpu_ctx):
     """accept_tri (four compares, the reference's :132 minus the implied u <= 1) and accept_tri_w (minimum3 form
     used by the pair test) decide identically on special and random (u, v)."""

@@ -124,14 +124,40 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b)
 {
     return mk3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
-__device__ __forceinline__ f3 normalize(f3 v) { return v / sqrtf(dot(v, v)); }
+/* Correctly rounded sqrt. hipcc's sqrtf is v_sqrt_f32 (not correctly rounded alone) + a one-ulp correction from two
+ * FMA residuals, wrapped in a 2^32 scaling for inputs below 2^-96 and a zero/infinity class fixup: 17 VALU. For
+ * x >= 2^-96 (including +inf) the correction alone is the IEEE square root -- checked against sqrtf over every such
+ * input on the device (selftest fn 15) -- so that range takes the 9-VALU core and everything else (tiny, zero,
+ * negative, NaN) the full sequence. WCPT_SQRT_CORE=0 uses sqrtf everywhere. */
+#ifndef WCPT_SQRT_CORE
+#define WCPT_SQRT_CORE 1
+#endif
+__device__ __forceinline__ float sqrt_core(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float s_dn = __uint_as_float(__float_as_uint(s) - 1u);
+    const float s_up = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r_dn = __builtin_fmaf(-s_dn, s, x);
+    const float r_up = __builtin_fmaf(-s_up, s, x);
+    float r = (r_dn <= 0.0f) ? s_dn : s;
+    r = (r_up > 0.0f) ? s_up : r;
+    return r;
+}
+__device__ __forceinline__ float sqrt_exact(float x)
+{
+#if WCPT_SQRT_CORE
+    if (__builtin_expect(x >= 0x1p-96f, 1)) return sqrt_core(x);
+#endif
+    return sqrtf(x);
+}
+__device__ __forceinline__ f3 normalize(f3 v) { return v / sqrt_exact(dot(v, v)); }
 __device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
 __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)
 {
     const float d = dot(N, I);
     const float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return mk3(0.0f, 0.0f, 0.0f);
-    return eta * I - N * (eta * d + sqrtf(k));
+    return eta * I - N * (eta * d + sqrt_exact(k));
 }
 __device__ __forceinline__ float sign1(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 __device__ __forceinline__ f3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
@@ -164,7 +190,7 @@ __device__ __forceinline__ float rand_f(uint32_t& state)
 __device__ __forceinline__ float RandomValueNormalDistribution(uint32_t& seed)
 {
     const float theta = 2.0f * kPI * rand_f(seed);
-    const float rho = sqrtf(-2.0f * wcpt_logf_rand(rand_f(seed))); /* == wcpt_logf on rand()'s values */
+    const float rho = sqrt_exact(-2.0f * wcpt_logf_rand(rand_f(seed))); /* == wcpt_logf on rand()'s values */
     return rho * wcpt_cosf_2pi(theta);                              /* == wcpt_cosf on [0, 2*pi] */
 }
 __device__ __forceinline__ f3 RandomDirection(uint32_t& seed)
@@ -241,7 +267,7 @@ __device__ __forceinline__ float raySphereNear(const Ray& r, f3 position, float 
     const float c = dot(oc, oc) - radius * radius;
     const float t = b * b - c;
     if (t < 0.0f) return -1.0f;
-    return -b - sqrtf(t);
+    return -b - sqrt_exact(t);
 }
 
 /* The acceptance test of :132 without its `u <= 1` term, which the other terms imply: with v >= 0, u + v >= u
@@ -765,7 +791,7 @@ __device__ __forceinline__ float CalculateReflectance(f3 inDir, f3 normal, float
     const float cosAngleIn = -dot(inDir, normal);
     const float sinSqr = refractRatio * refractRatio * (1.0f - cosAngleIn * cosAngleIn);
     if (sinSqr >= 1.0f) return 1.0f;
-    const float cosRefr = sqrtf(1.0f - sinSqr);
+    const float cosRefr = sqrt_exact(1.0f - sinSqr);
     const float dPerp = iorA * cosAngleIn + iorB * cosRefr;
     const float dPar = iorB * cosAngleIn + iorA * cosRefr;
     if (fminf(dPerp, dPar) < 1e-8f) return 1.0f;
@@ -802,6 +828,9 @@ __device__ __forceinline__ void path_begin(PathState& ps, f3 origin, f3 dir)
     ps.bounce = 0;
 }
 
+#ifndef WCPT_SHADE_SHARED
+#define WCPT_SHADE_SHARED 1
+#endif
 /* Shading after an Intersect (pathTracer.comp:248-280). Returns true when the path is finished, with its
  * radiance in L: on a miss (:248-249) or when the bounce loop is exhausted (:245, :283). */
 __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t& rng, const wcpt_scene_data& sd,
@@ -819,6 +848,41 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
     const float roughness = m.roughness;
     ps.totalLight = ps.totalLight + (emission * emissionStrength) * ps.transmittance;
 
+#if WCPT_SHADE_SHARED
+    /* Both branches of :256-280 end in normalize(base + roughness * RandomDirection(rng)) and a new 1/direction.
+     * That tail is shared here, after the dielectric-only part (Fresnel, refract and the :273 rand, which must
+     * precede RandomDirection in the lane's RNG sequence), so a wave whose lanes hit both kinds of material runs
+     * RandomDirection (6 rand, 3 log, 3 cos, 4 sqrt) once instead of once per branch. Every lane performs the
+     * reference's operations in the reference's order. */
+    const bool metal = mtype == WCPT_MATERIAL_METAL;
+    const f3 R = reflect(ray.direction, h.normal);
+    f3 base = R;
+    bool followReflection = true;
+    if (!metal) {
+        const float ior = m.ior;
+        const float etaI = h.front ? 1.0f : ior;
+        const float etaT = h.front ? ior : 1.0f;
+        const float reflectProb = CalculateReflectance(ray.direction, h.normal, etaI, etaT);
+        const f3 T = refract(ray.direction, h.normal, etaI / etaT);
+        followReflection = (T.x == 0.0f && T.y == 0.0f && T.z == 0.0f);
+        if (!followReflection) followReflection = (rand_f(rng) <= reflectProb); /* :273 short-circuit */
+        if (!followReflection) base = T;
+    }
+    const f3 rd = RandomDirection(rng);
+    const f3 dir = normalize(base + roughness * rd);
+    if (metal) {
+        ray.origin = h.p + h.normal * kBias;                                  /* :257 */
+        ps.transmittance = ps.transmittance * ld3(m.albedo);                  /* :261 */
+    } else {
+        if (!followReflection && !h.front) {                                  /* :276-278 */
+            const f3 e = ((ld3(m.absorption) * -1.0f) * m.absorptionStrength) * h.t;
+            ps.transmittance = ps.transmittance * mk3(wcpt_expf(e.x), wcpt_expf(e.y), wcpt_expf(e.z));
+        }
+        ray.origin = h.p + (kBias * h.normal) * sign1(dot(dir, h.normal));   /* :279 */
+    }
+    ray.direction = dir;
+    ray.invDirection = rcp3(dir);
+#else
     if (mtype == WCPT_MATERIAL_METAL) {
         ray.origin = h.p + h.normal * kBias;
         const f3 R = reflect(ray.direction, h.normal);
@@ -844,6 +908,7 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
         }
         ray.origin = h.p + (kBias * h.normal) * sign1(dot(ray.direction, h.normal));
     }
+#endif
     ps.bounce++;
     if (ps.bounce > sd.maxBounceCount) { /* loop exhausted: no sky term (:283) */
         L = ps.totalLight;

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
     case 2: out[i] = __float_as_uint(wcpt_logf(__uint_as_float(a))); break;
     case 3: out[i] = __float_as_uint(wcpt_cosf(__uint_as_float(a))); break;
     case 4: out[i] = __float_as_uint(wcpt_expf(__uint_as_float(a))); break;
-    case 5: out[i] = __float_as_uint(sqrtf(__uint_as_float(a))); break;
+    case 5: out[i] = __float_as_uint(sqrt_exact(__uint_as_float(a))); break;
     case 6: out[i] = __float_as_uint(__uint_as_float(a) / __uint_as_float(in2[i])); break;
     case 8: { /* exhaustive fast-reciprocal check: mismatches of rcp_exact's fast path vs IEEE 1/x over the 2^16
                  inputs (a << 16) | k inside the fast path's range */
@@ -260,6 +260,17 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
         const float u = __uint_as_float(a), v = __uint_as_float(in2[i]);
         const float uv = u + v;
         out[i] = (accept_tri(1.0f, u, v, uv) ? 1u : 0u) | (accept_tri_w(1.0f, u, v, 1.0f - uv) ? 2u : 0u);
+        break;
+    }
+    case 15: { /* the kernels' sqrt (sqrt_exact) vs hipcc's correctly rounded sqrtf over the 2^16 inputs (a << 16) | k:
+                  mismatches, NaN == NaN */
+        uint32_t bad = 0;
+        for (uint32_t k = 0; k < 65536u; k++) {
+            const float x = __uint_as_float((a << 16) | k);
+            const float r = sqrt_exact(x), q = sqrtf(x);
+            bad += (__float_as_uint(r) != __float_as_uint(q) && !(r != r && q != q)) ? 1u : 0u;
+        }
+        out[i] = bad;
         break;
     }
     case 7: { /* RandomDirection: 3 words per input */
