@@ -193,12 +193,93 @@ __device__ __forceinline__ float RandomValueNormalDistribution(uint32_t& seed)
     const float rho = sqrt_exact(-2.0f * wcpt_logf_rand(rand_f(seed))); /* == wcpt_logf on rand()'s values */
     return rho * wcpt_cosf_2pi(theta);                              /* == wcpt_cosf on [0, 2*pi] */
 }
+/* wcpt_libm.h's wcpt_logf_rand and wcpt_cosf_2pi on two arguments at once: the same binary32 operations in the same
+ * order per half, with the float arithmetic on packed FP32 instructions (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32
+ * for the reciprocal's Newton step) and the integer and rounding steps per half. Bit-identical to the scalar
+ * functions (and so to the oracle) by construction; selftest fn 7 checks RandomDirection against the oracle. */
+#ifndef WCPT_RANDDIR_PAIRS
+#define WCPT_RANDDIR_PAIRS 1
+#endif
+__device__ __forceinline__ v2f bcast2(float s) { v2f r = {s, s}; return r; }
+__device__ __forceinline__ v2f logf_rand2(v2f x)
+{
+    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
+    const float Lg1 = 0.66666662693f, Lg2 = 0.40000972152f, Lg3 = 0.28498786688f, Lg4 = 0.24279078841f;
+    uint32_t ix0 = __float_as_uint(x.x) + (0x3f800000u - 0x3f3504f3u);
+    uint32_t ix1 = __float_as_uint(x.y) + (0x3f800000u - 0x3f3504f3u);
+    const int k0 = (int)(ix0 >> 23) - 127, k1 = (int)(ix1 >> 23) - 127;
+    ix0 = (ix0 & 0x007fffffu) + 0x3f3504f3u;
+    ix1 = (ix1 & 0x007fffffu) + 0x3f3504f3u;
+    const v2f m = {__uint_as_float(ix0), __uint_as_float(ix1)};
+    const v2f f = m - bcast2(1.0f);
+    const v2f den = bcast2(2.0f) + f;
+    v2f y;
+    y.x = __builtin_amdgcn_rcpf(den.x);
+    y.y = __builtin_amdgcn_rcpf(den.y);
+    const v2f e = __builtin_elementwise_fma(-den, y, bcast2(1.0f));
+    const v2f rc = __builtin_elementwise_fma(e, y, y); /* wcpt_rcp1_2 per half */
+    const v2f sv = f * rc;
+    const v2f z = sv * sv;
+    const v2f w = z * z;
+    const v2f t1 = w * (bcast2(Lg2) + w * bcast2(Lg4));
+    const v2f t2 = z * (bcast2(Lg1) + w * bcast2(Lg3));
+    const v2f R = t2 + t1;
+    const v2f hfsq = bcast2(0.5f) * f * f;
+    const v2f dk = {(float)k0, (float)k1};
+    v2f out = sv * (hfsq + R) + dk * bcast2(ln2_lo) - hfsq + f + dk * bcast2(ln2_hi);
+    if (x.x == 0.0f) out.x = __uint_as_float(0xff800000u);
+    if (x.y == 0.0f) out.y = __uint_as_float(0xff800000u);
+    return out;
+}
+__device__ __forceinline__ float cos_quadrant(int j, float c, float s)
+{
+    switch (j & 3) {
+    case 0: return c;
+    case 1: return -s;
+    case 2: return -c;
+    default: return s;
+    }
+}
+__device__ __forceinline__ v2f cosf_2pi2(v2f ax)
+{
+    const float two_over_pi = 0.63661977236758134f;
+    const float pio2_1 = 1.5703125f, pio2_2 = 4.837512969970703125e-4f, pio2_3 = 7.5497899548e-8f;
+    const float S1 = -1.6666654611e-1f, S2 = 8.3321608736e-3f, S3 = -1.9515295891e-4f;
+    const float C1 = 4.166664568298827e-2f, C2 = -1.388731625493765e-3f, C3 = 2.443315711809948e-5f;
+    const v2f q = ax * bcast2(two_over_pi) + bcast2(0.5f);
+    const v2f jf = {floorf(q.x), floorf(q.y)};
+    const int j0 = (int)jf.x, j1 = (int)jf.y;
+    const v2f r = ((ax - jf * bcast2(pio2_1)) - jf * bcast2(pio2_2)) - jf * bcast2(pio2_3);
+    const v2f z = r * r;
+    v2f c = ((bcast2(C3) * z + bcast2(C2)) * z + bcast2(C1)) * z * z;
+    c = c - bcast2(0.5f) * z;
+    c = c + bcast2(1.0f);
+    v2f sn = ((bcast2(S3) * z + bcast2(S2)) * z + bcast2(S1)) * z * r;
+    sn = sn + r;
+    v2f out;
+    out.x = cos_quadrant(j0, c.x, sn.x);
+    out.y = cos_quadrant(j1, c.y, sn.y);
+    return out;
+}
 __device__ __forceinline__ f3 RandomDirection(uint32_t& seed)
 {
+#if WCPT_RANDDIR_PAIRS
+    /* Random.glsl:43-56 with the draws in the reference order: theta_x, rho_x, theta_y, rho_y, theta_z, rho_z */
+    const float ux0 = rand_f(seed), ux1 = rand_f(seed);
+    const float uy0 = rand_f(seed), uy1 = rand_f(seed);
+    const v2f theta = bcast2(2.0f * kPI) * (v2f){ux0, uy0};
+    const v2f lg = logf_rand2((v2f){ux1, uy1});
+    const v2f m2 = bcast2(-2.0f) * lg;
+    const v2f rho = {sqrt_exact(m2.x), sqrt_exact(m2.y)};
+    const v2f xy = rho * cosf_2pi2(theta);
+    const float z = RandomValueNormalDistribution(seed);
+    return normalize(mk3(xy.x, xy.y, z));
+#else
     const float x = RandomValueNormalDistribution(seed);
     const float y = RandomValueNormalDistribution(seed);
     const float z = RandomValueNormalDistribution(seed);
     return normalize(mk3(x, y, z));
+#endif
 }
 
 /* ---- pathTracer.comp:24-28, 50-58 ------------------------------------------------------------- */
@@ -268,6 +349,47 @@ __device__ __forceinline__ float raySphereNear(const Ray& r, f3 position, float 
     const float t = b * b - c;
     if (t < 0.0f) return -1.0f;
     return -b - sqrt_exact(t);
+}
+
+/* The sphere loop of Intersect (pathTracer.comp:140-149) over spheres [0, count): the near root of each, accepted
+ * iff 0 < t < rec.t, in sphere order. WCPT_SPHERE_PAIRS=1 (default) evaluates two spheres per step with packed
+ * FP32 (v_pk_mul_f32 / v_pk_add_f32: per half exactly raySphereNear's binary32 operations), the square roots and
+ * the ordered takes per sphere. */
+constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
+#ifndef WCPT_SPHERE_PAIRS
+#define WCPT_SPHERE_PAIRS 1
+#endif
+__device__ __forceinline__ void sphere_loop(const Ray& r, uint32_t count, const wcpt_sphere* __restrict__ spheres,
+                                            float& rt, uint32_t& prim)
+{
+    uint32_t i = 0;
+#if WCPT_SPHERE_PAIRS
+    const v2f ox = {r.origin.x, r.origin.x}, oy = {r.origin.y, r.origin.y}, oz = {r.origin.z, r.origin.z};
+    const v2f dx = {r.direction.x, r.direction.x}, dy = {r.direction.y, r.direction.y},
+                dz = {r.direction.z, r.direction.z};
+    for (; i + 1u < count; i += 2u) {
+        const wcpt_sphere& s0 = spheres[i];
+        const wcpt_sphere& s1 = spheres[i + 1u];
+        const v2f cx = {s0.position[0], s1.position[0]}, cy = {s0.position[1], s1.position[1]},
+                    cz = {s0.position[2], s1.position[2]}, rad = {s0.radius, s1.radius};
+        const v2f ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;     /* oc = origin - position */
+        const v2f b = (ocx * dx + ocy * dy) + ocz * dz;           /* dot(oc, d) */
+        const v2f c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - rad * rad;
+        const v2f t = b * b - c;
+        const float t0 = t.x < 0.0f ? -1.0f : -b.x - sqrt_exact(t.x);
+        const float t1 = t.y < 0.0f ? -1.0f : -b.y - sqrt_exact(t.y);
+        if (t0 > 0.0f && t0 < rt) { rt = t0; prim = kSpherePrim | i; }
+        if (t1 > 0.0f && t1 < rt) { rt = t1; prim = kSpherePrim | (i + 1u); }
+    }
+#endif
+    for (; i < count; i++) {
+        const wcpt_sphere& s = spheres[i];
+        const float tempRec = raySphereNear(r, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
+        if (tempRec > 0.0f && tempRec < rt) {
+            rt = tempRec;
+            prim = kSpherePrim | i;
+        }
+    }
 }
 
 /* The acceptance test of :132 without its `u <= 1` term, which the other terms imply: with v >= 0, u + v >= u
@@ -442,6 +564,25 @@ __device__ __forceinline__ uint32_t leaf_record(uint32_t first, uint32_t count, 
 #endif
 constexpr int kPhaseTimers = 8;
 
+/* Cost attribution (tools only, tools/ab_build.sh): WCPT_DUP_<part>=1 evaluates that part a second time on
+ * laundered inputs and discards the result, so the A/B time difference is the part's cost. Never on by default. */
+#ifndef WCPT_DUP_SPHERES
+#define WCPT_DUP_SPHERES 0
+#endif
+#ifndef WCPT_DUP_RANDDIR
+#define WCPT_DUP_RANDDIR 0
+#endif
+#ifndef WCPT_DUP_PAIR
+#define WCPT_DUP_PAIR 0
+#endif
+#ifndef WCPT_DUP_BOX
+#define WCPT_DUP_BOX 0
+#endif
+__device__ __forceinline__ float launder(float x) { asm volatile("" : "+v"(x)); return x; }
+__device__ __forceinline__ uint32_t launder_u(uint32_t x) { asm volatile("" : "+v"(x)); return x; }
+__device__ __forceinline__ void sink(float x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void sink_u(uint32_t x) { asm volatile("" ::"v"(x)); }
+
 /* Per-lane work counters; reduced per wave and added to global u64 counters. */
 struct Counters {
     uint32_t pixels, segments, sphere_tests, node_pops, interior_visits, triangle_tests, hits, draw_fetches;
@@ -565,7 +706,6 @@ struct LdsStack {
 /* Closest-hit record during traversal: (t, primitive) only; the winner's normal and material are rebuilt
  * once afterwards (resolve_hit) with the reference's expressions, which gives the values the reference
  * computes at each update (:145, :173) without paying a normalize per closer hit. */
-constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 
 /* Geometric normal of the triangle at index positions prim..prim+2 of draw `draw` (:173): from its single record
  * when the triangle starts on a triangle boundary inside the records (the record was derived from exactly these
@@ -631,16 +771,24 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
     }
 
-    for (uint32_t i = 0; i < sd.sphereCount; i++) {
-        const wcpt_sphere& s = spheres[i];
-        const f3 sp = mk3(s.position[0], s.position[1], s.position[2]);
-        const float tempRec = raySphereNear(ray, sp, s.radius);
-        if (COUNT) cnt.sphere_tests++;
-        if (tempRec > 0.0f && tempRec < rt) {
-            rt = tempRec;
-            prim = kSpherePrim | i;
+    sphere_loop(ray, sd.sphereCount, spheres, rt, prim);
+    if (COUNT) cnt.sphere_tests += sd.sphereCount;
+#if WCPT_DUP_SPHERES
+    {
+        Ray r2 = ray;
+        r2.origin.x = launder(r2.origin.x);
+        r2.direction.x = launder(r2.direction.x);
+        float rt2 = kInfinity;
+        uint32_t p2 = 0;
+        for (uint32_t i = 0; i < sd.sphereCount; i++) {
+            const wcpt_sphere& s = spheres[i];
+            const float tr = raySphereNear(r2, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
+            if (tr > 0.0f && tr < rt2) { rt2 = tr; p2 = i; }
         }
+        sink(rt2);
+        sink_u(p2);
     }
+#endif
     phase_mark(cnt, 1);
 
     for (uint32_t i = 0; i < sd.drawCommandCount; i++) {
@@ -687,6 +835,15 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                         uint32_t off = (k >> 1) * kPairRecordBytes, tag = kNoTag;
                         for (; off < offEnd; off += kPairRecordBytes) {
                             const PairHit ph = rayTrianglePair(ray, load_pair_at(pbase, off));
+#if WCPT_DUP_PAIR
+                            {
+                                Ray r2 = ray;
+                                r2.origin.x = launder(r2.origin.x);
+                                const PairHit p2 = rayTrianglePair(r2, load_pair_at(pbase, off));
+                                sink(p2.t.x + p2.t.y);
+                                sink_u((p2.hit0 ? 1u : 0u) | (p2.hit1 ? 2u : 0u));
+                            }
+#endif
                             count_tri<COUNT, DIAG>(cnt);
                             if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
                             count_tri<COUNT, DIAG>(cnt);
@@ -733,6 +890,18 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 float l0, l1, r0, r1;
                 node_box(ray, L, l0, l1);
                 node_box(ray, R, r0, r1);
+#if WCPT_DUP_BOX
+                {
+                    Ray r2 = ray;
+                    r2.origin.x = launder(r2.origin.x);
+                    r2.origin.y = launder(r2.origin.y);
+                    r2.origin.z = launder(r2.origin.z);
+                    float a0, a1, b0, b1;
+                    node_box(r2, L, a0, a1);
+                    node_box(r2, R, b0, b1);
+                    sink(a0 + a1 + b0 + b1);
+                }
+#endif
                 if (COUNT) {
                     cnt.interior_visits++;
                     cnt.node_pops += 2;
@@ -869,6 +1038,13 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
         if (!followReflection) base = T;
     }
     const f3 rd = RandomDirection(rng);
+#if WCPT_DUP_RANDDIR
+    {
+        uint32_t r2 = launder_u(rng);
+        const f3 d2 = RandomDirection(r2);
+        sink(d2.x + d2.y + d2.z);
+    }
+#endif
     const f3 dir = normalize(base + roughness * rd);
     if (metal) {
         ray.origin = h.p + h.normal * kBias;                                  /* :257 */

@@ -54,14 +54,7 @@ __device__ __forceinline__ void segment_prologue(const Ray& r, const wcpt_scene_
 {
     rt = kInfinity;
     prim = kNoPrim;
-    for (uint32_t i = 0; i < sd.sphereCount; i++) {
-        const wcpt_sphere& s = spheres[i];
-        const float tempRec = raySphereNear(r, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
-        if (tempRec > 0.0f && tempRec < rt) {
-            rt = tempRec;
-            prim = kSpherePrim | i;
-        }
-    }
+    sphere_loop(r, sd.sphereCount, spheres, rt, prim);
     if (COUNT) {
         cnt.segments++;
         cnt.sphere_tests += sd.sphereCount;
