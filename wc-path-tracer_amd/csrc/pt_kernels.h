@@ -13,8 +13,11 @@ namespace wcpt {
  * midpoint BVH can overflow; our far-child stack needs at most (tree depth - 1) entries. Deeper trees set
  * the WCPT_ERROR_STACK_OVERFLOW status instead of writing out of bounds. */
 constexpr int kPrivateStack = 48;          /* stack kind 0: all entries in scratch                         */
-constexpr int kLdsStack = 16;              /* stack kind 1: entries in LDS (16 x 8 B x 64 lanes = 8 KiB/wave) */
-constexpr int kSpillStack = 32;            /*               + entries 16..47 spilled to scratch              */
+#ifndef WCPT_MK_LDS_STACK
+#define WCPT_MK_LDS_STACK 16
+#endif
+constexpr int kLdsStack = WCPT_MK_LDS_STACK; /* stack kind 1: entries in LDS (16 x 8 B x 64 lanes = 8 KiB/wave) */
+constexpr int kSpillStack = 48 - kLdsStack;  /*               + entries 16..47 spilled to scratch              */
 constexpr int kStackDepth = kLdsStack + kSpillStack;
 
 struct LaunchArgs {
