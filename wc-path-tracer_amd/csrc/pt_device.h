@@ -455,6 +455,7 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { r
  * Per-draw table entry: {single record address, pair record address, triangle count, flags} (4 x u64). */
 constexpr uint32_t kTriTableWords = 4;
 constexpr uint64_t kTriFlagPackedRefs = 1u; /* table word 3: stack entries may carry (left, count) */
+constexpr uint64_t kTriFlagIndex24 = 2u;    /* table word 3: the draw's indexCount is < 2^24 */
 typedef const WCPT_GLOBAL v4f* gtri_ptr;
 struct TriE { f3 a, e1, e2; };
 __device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
@@ -553,6 +554,33 @@ __device__ __forceinline__ uint32_t leaf_record(uint32_t first, uint32_t count, 
 {
     const uint32_t k = first / 3u;
     return (k * 3u == first && (uint64_t)k + (count + 2u) / 3u <= ntri) ? k : kNoRecord;
+}
+/* The same validity as a byte offset into the single records (48 B per triangle = 16 B per index position, so the
+ * leaf's first record is at 16 * first), without a division: for first < 2^24 (draws with kTriFlagIndex24),
+ * first % 3 == 0 exactly when (first * 0xAAAAAB) mod 2^24 <= 0x555555 (0xAAAAAB is the inverse of 3 mod 2^24; checked
+ * for every first < 2^24), one full-rate v_mul_u32_u24 instead of leaf_record's quarter-rate v_mul_hi_u32 pair.
+ * The end test first + count + 2 <= 3 * ntri is leaf_record's for counts that are multiples of 3 (the reference's)
+ * and at most stricter otherwise (such a leaf takes the index path). lim3 = 3 * ntri. */
+__device__ __forceinline__ uint32_t leaf_record_off24(uint32_t first, uint32_t count, uint32_t lim3)
+{
+    const bool aligned = (__umul24(first, 0xAAAAABu) & 0xFFFFFFu) <= 0x555555u;
+    return (aligned && first + count + 2u <= lim3) ? first * 16u : kNoRecord;
+}
+/* leaf_record as a byte offset for any draw (records beyond 4 GiB take the index path) */
+__device__ __forceinline__ uint32_t leaf_record_off(uint32_t first, uint32_t count, uint32_t ntri)
+{
+    const uint32_t k = leaf_record(first, count, ntri);
+    return (k != kNoRecord && k < (1u << 26)) ? k * 48u : kNoRecord;
+}
+__device__ __forceinline__ TriE load_tri_at(gtri_ptr t, uint32_t off)
+{
+    const gtri_ptr q = reinterpret_cast<gtri_ptr>(reinterpret_cast<const WCPT_GLOBAL char*>(t) + off);
+    const v4f r0 = q[0], r1 = q[1], r2 = q[2];
+    TriE e;
+    e.a = mk3(r0.x, r0.y, r0.z);
+    e.e1 = mk3(r0.w, r1.x, r1.y);
+    e.e2 = mk3(r1.z, r1.w, r2.x);
+    return e;
 }
 
 /* Megakernel phase timers (tools only: a library built with -DWCPT_MK_TIMERS=1, tools/mk_phases.py). Each wave

@@ -157,10 +157,15 @@ constexpr int wf_lds_per_wave(int n) { return n * 512; }
 constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
 
+#ifndef WCPT_WF_REC_OFF24
+#define WCPT_WF_REC_OFF24 1
+#endif
 struct Geom {
     gtri_ptr tris;
     uint32_t ntri;
-    bool packed; /* stack entries carry (left, count): kTriFlagPackedRefs */
+    uint32_t lim3; /* 3 * ntri (kTriFlagIndex24 draws) */
+    bool packed;   /* stack entries carry (left, count): kTriFlagPackedRefs */
+    bool idx24;    /* index positions < 2^24: kTriFlagIndex24 */
     gnode_ptr bvh;
     gu32_ptr indices;
     gf32_ptr vertices;
@@ -173,6 +178,8 @@ __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ 
     g.tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * d];      /* single records */
     g.ntri = (uint32_t)tri_records[kTriTableWords * d + 2u];
     g.packed = (tri_records[kTriTableWords * d + 3u] & kTriFlagPackedRefs) != 0u;
+    g.idx24 = WCPT_WF_REC_OFF24 && (tri_records[kTriTableWords * d + 3u] & kTriFlagIndex24) != 0u;
+    g.lim3 = 3u * g.ntri;
     g.bvh = as_nodes(draws[d].bvhBuffer);
     g.indices = as_u32(draws[d].indexBuffer);
     g.vertices = as_f32(draws[d].vertexBuffer);
@@ -194,13 +201,13 @@ __device__ __forceinline__ void diag_mark(uint64_t* tim, uint64_t& tprev, int k)
 }
 
 /* Node cursor: interior -> (a = left child index); leaf -> (a = current index position, b = end position,
- * r = record of the current triangle or kNoRecord). */
-__device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, uint32_t ntri, uint32_t& a, uint32_t& b,
+ * r = byte offset of the current triangle's single record or kNoRecord). */
+__device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, const Geom& g, uint32_t& a, uint32_t& b,
                                             uint32_t& r, uint32_t& mode)
 {
     a = left;
     b = left + count;
-    r = leaf_record(left, count, ntri);
+    r = g.idx24 ? leaf_record_off24(left, count, g.lim3) : leaf_record_off(left, count, g.ntri);
     mode = count > 0 ? kModeLeaf : kModeInterior;
 }
 
@@ -222,7 +229,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     stk.sp = 0;
     Counters cnt = {};
     bool overflow = false;
-    Geom g0 = {nullptr, 0u, false, nullptr, nullptr, nullptr}, gl = {nullptr, 0u, false, nullptr, nullptr, nullptr};
+    Geom g0 = {nullptr, 0u, 0u, false, false, nullptr, nullptr, nullptr}, gl = g0;
     if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
 
     bool has = false, drained = false;
@@ -253,7 +260,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             float c0, c1;
             node_box(ray, root, c0, c1);
             if (c0 > c1 || c1 < 0.0f || c0 > rt) continue;
-            cursor_from(root.b.z, root.b.w, g.ntri, ca, cb, cr, mode);
+            cursor_from(root.b.z, root.b.w, g, ca, cb, cr, mode);
             stk.reset();
             return;
         }
@@ -320,7 +327,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     stk.pop(ni, t0);
                     if (t0 > rt) continue;
                     const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
-                    cursor_from(lc.x, lc.y, g.ntri, ca, cb, cr, mode);
+                    cursor_from(lc.x, lc.y, g, ca, cb, cr, mode);
                     found = true;
                     break;
                 }
@@ -355,7 +362,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 }
                 if (passNear && !((leftFirst ? l0 : r0) > rt)) {
                     const uint32_t nl = leftFirst ? L.b.z : R.b.z, nc = leftFirst ? L.b.w : R.b.w;
-                    cursor_from(nl, nc, g.ntri, ca, cb, cr, mode);
+                    cursor_from(nl, nc, g, ca, cb, cr, mode);
                 } else {
                     mode = kModePop;
                 }
@@ -364,7 +371,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             if (has && mode == kModeLeaf) {
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
-                const TriE tr = cr != kNoRecord ? load_tri(g.tris, cr) : tri_from_indices(g.indices, g.vertices, ca);
+                const TriE tr = cr != kNoRecord ? load_tri_at(g.tris, cr) : tri_from_indices(g.indices, g.vertices, ca);
                 const float tt = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
                 if (COUNT) {
                     cnt.triangle_tests++;
@@ -376,7 +383,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     primDraw = d;
                 }
                 ca += 3;
-                cr += (cr != kNoRecord) ? 1u : 0u;
+                cr += (cr != kNoRecord) ? 48u : 0u;
                 if (ca >= cb) mode = kModePop;
             }
             diag_mark<DIAG>(tim, tprev, 1);

@@ -308,7 +308,8 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
          * bits (pt_device.h node_ref); unknown BVH size -> node-index entries */
         Buffer* bb = buffer_at(ctx, dc[d].bvhBuffer, o);
         const uint64_t nodes = bb ? (bb->bytes - o) / sizeof(wcpt_node) : ~0ull;
-        const uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
+        uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
+        if (dc[d].indexCount < (1u << 24)) flags |= 2u; /* pt_device.h kTriFlagIndex24 */
         const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, flags};
         for (uint64_t w = 0; w < W; w++) {
             if (ctx->tri_table[W * d + w] != entry[w]) {
