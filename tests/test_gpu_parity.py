@@ -420,6 +420,60 @@ def test_record_formats_match_oracle(gpu_ctx, pairs, name, W, H):
     assert cnt == rcnt
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("pairs", [0, 1])
+@pytest.mark.parametrize("combo", ["atrium_twice", "cornell_then_atrium"])
+def test_multi_draw_deep_trees_match_oracle(gpu_ctx, kernel, pairs, combo):
+    """Several draw commands over deep BVHs (:151-201: the next draw's traversal starts with the stack of the previous
+    one exhausted, closest hit over all of them, ties to the earlier draw). The megakernel walks multiple draws in
+    one flat traversal loop; the atrium's 33-level midpoint tree drives its stacks into the scratch spill."""
+    import copy
+    s = copy.copy(get_scene("atrium"))
+    atrium = s.meshes[0]
+    s.meshes = [atrium, atrium] if combo == "atrium_twice" else [get_scene("cornell").meshes[0], atrium]
+    W, H = 48, 32
+    gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, pairs)
+    try:
+        img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=3, kernel=kernel)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, -1)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=3, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+
+
+@pytest.mark.parametrize("pairs", [0, 1])
+@pytest.mark.parametrize("stack", [0, 1])
+def test_megakernel_atrium_rows_all_modes(gpu_ctx, pairs, stack):
+    """A 1920-wide atrium band through the render, counting and diagnostic megakernel builds (the diagnostic build
+    adds wave-level ballots inside the traversal): none may report a stack overflow, the render must equal the
+    oracle and the counters of both counting builds must agree. Regression test for the toolchain mis-compile of
+    the nested draw loop."""
+    s = get_scene("atrium")
+    W, H, y0, rows = 1920, 1080, 520, 8
+    gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, pairs)
+    gpu_ctx.set_option(wcpt._lib.OPTION_STACK, stack)
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    try:
+        gpu_ctx.create_screen(W, H)
+        gpu_ctx.set_row_range(y0, rows)
+        sd = s.scene_data(W, H, max_bounce=4, samples=1, frame=0)
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()
+        img = gpu_ctx.readback(rows)
+        cnt = gpu_ctx.render_counters(sd, *dev.addresses())
+        dcnt = gpu_ctx.render_counters(sd, *dev.addresses(), diagnostics=True)
+    finally:
+        gpu_ctx.set_row_range(0, 0)
+        gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, -1)
+        gpu_ctx.set_option(wcpt._lib.OPTION_STACK, 1)
+        dev.free()
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=4, y0=y0, rows=rows, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+    assert {k: dcnt[k] for k in cnt} == cnt
+
+
 # ---- composite.comp (display step, SURVEY.md §8(f) row 4) ---------------------------------------------------
 @pytest.mark.parametrize("rgba8", [False, True])
 def test_composite_matches_oracle(gpu_ctx, rgba8):

@@ -485,12 +485,29 @@ __device__ __forceinline__ TriPair load_pair(gtri_ptr t, uint32_t j)
 /* The pair record at byte offset `off` from the record base (pair j at off = 80 j). */
 constexpr uint32_t kPairRecordBytes = 16u * kPairRecordFloat4s;
 constexpr uint32_t kNoTag = 0xFFFFFFFFu;
-#ifndef WCPT_PAIR_OFFSET_LOOP
-#define WCPT_PAIR_OFFSET_LOOP 1
+#ifndef WCPT_PAIR_UNIFORM
+#define WCPT_PAIR_UNIFORM 1
 #endif
+
 __device__ __forceinline__ TriPair load_pair_at(const WCPT_GLOBAL char* base, uint32_t off)
 {
     const gtri_ptr q = reinterpret_cast<gtri_ptr>(base + off);
+    const v4f r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    TriPair p;
+    p.ax = r0.xy;  p.ay = r0.zw;
+    p.az = r1.xy;  p.e1x = r1.zw;
+    p.e1y = r2.xy; p.e1z = r2.zw;
+    p.e2x = r3.xy; p.e2y = r3.zw;
+    p.e2z = r4.xy;
+    return p;
+}
+/* The same record through the constant address space (4): the records are read-only for the whole launch, and a
+ * wave-uniform offset then lowers to scalar loads (s_load_dwordx16 / s_load_dwordx4 through the scalar cache) whose
+ * values the packed-FP32 instructions read straight from SGPRs. */
+typedef const __attribute__((address_space(4))) v4f* ctri_ptr;
+__device__ __forceinline__ TriPair load_pair_const(const WCPT_GLOBAL char* base, uint32_t off)
+{
+    const ctri_ptr q = (ctri_ptr)(uintptr_t)(base + off);
     const v4f r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
     TriPair p;
     p.ax = r0.xy;  p.ay = r0.zw;
@@ -785,8 +802,217 @@ __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t pri
     return h;
 }
 
-/* pathTracer.comp:135-211. PAIRS: leaf tests on pair records (else single records). */
-template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
+/* One draw command's geometry (pathTracer.comp:152-156 and the derived records of its table entry). */
+struct DrawGeom {
+    gnode_ptr bvh;
+    gu32_ptr indices;
+    gf32_ptr vertices;
+    gtri_ptr tris; /* pair records (PAIRS) or single records */
+    uint32_t ntri;
+    bool packed; /* stack entries carry (left, count): kTriFlagPackedRefs */
+};
+template <bool PAIRS>
+__device__ __forceinline__ DrawGeom draw_geom(const wcpt_draw_command* __restrict__ draws,
+                                              const uint64_t* __restrict__ tri_records, uint32_t i)
+{
+    DrawGeom g;
+    g.bvh = as_nodes(draws[i].bvhBuffer);
+    g.indices = as_u32(draws[i].indexBuffer);
+    g.vertices = as_f32(draws[i].vertexBuffer);
+    g.tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + (PAIRS ? 1u : 0u)];
+    g.ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
+    g.packed = (tri_records[kTriTableWords * i + 3u] & kTriFlagPackedRefs) != 0u;
+    return g;
+}
+
+/* Leaf (:164-178): every triangle of the leaf at index positions [curLeft, curLeft + curCount), in index order,
+ * taken iff accepted with t < rec.t (strict). UNIFORM: the leaf's whole pairs may be read with scalar loads (the
+ * draw's record base must then be wave-uniform). */
+template <bool COUNT, bool DIAG, bool PAIRS, bool UNIFORM>
+__device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uint32_t curLeft, uint32_t curCount,
+                                          float& rt, uint32_t& prim, Counters& cnt)
+{
+    const uint32_t k0 = leaf_record(curLeft, curCount, g.ntri);
+    if (PAIRS && k0 != kNoRecord) {
+        /* triangles [k0, kend) in pair records (2j, 2j+1): a leaf that starts in the second slot of a pair tests
+         * that pair for its first triangle, then whole pairs, then possibly the first slot of a last pair -- no
+         * per-iteration slot checks; applied in index order, strict < */
+        const uint32_t kend = k0 + (curCount + 2u) / 3u;
+        uint32_t k = k0;
+        if (k & 1u) {
+            const PairHit ph = rayTrianglePair(ray, load_pair(g.tris, k >> 1));
+            count_tri<COUNT, DIAG>(cnt);
+            if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
+            k++;
+        }
+        /* whole pairs: one 32-bit byte-offset induction variable from the draw's record base, and the winner
+         * recorded as a tag -- the pair's offset for its first triangle, offset + 1 for its second -- decoded into
+         * the index position once per leaf */
+        const uint32_t kfull = kend & ~1u;
+        const WCPT_GLOBAL char* pbase = reinterpret_cast<const WCPT_GLOBAL char*>(g.tris);
+        const uint32_t offEnd = (kfull >> 1) * kPairRecordBytes;
+        uint32_t off = (k >> 1) * kPairRecordBytes, tag = kNoTag;
+#if WCPT_PAIR_UNIFORM
+        if (UNIFORM) {
+            /* Lanes whose whole-pair range equals the first active lane's (in a coherent wave: all of them) read
+             * the records at that lane's offset with scalar loads: the offset is re-derived each iteration with
+             * readfirstlane, so the loads are wave-uniform, go through the scalar cache (no per-lane addresses, no
+             * vector-memory return of 64 copies of the record) and the packed-FP32 instructions take the record
+             * straight from SGPRs (c2 -8%). The loop stays an ordinary per-lane loop. The other lanes take the
+             * per-lane loop below. */
+            const uint32_t offU = __builtin_amdgcn_readfirstlane(off);
+            const uint32_t endU = __builtin_amdgcn_readfirstlane(offEnd);
+            /* tested through an opaque value: a plain `off == offU` lets the compiler substitute the equal
+             * per-lane value back into the loads */
+            uint32_t diff = (off ^ offU) | (offEnd ^ endU);
+            asm volatile("" : "+v"(diff));
+            if (diff == 0u) {
+                for (; off < offEnd; off += kPairRecordBytes) {
+                    const PairHit ph = rayTrianglePair(ray, load_pair_const(pbase, __builtin_amdgcn_readfirstlane(off)));
+                    count_tri<COUNT, DIAG>(cnt);
+                    if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
+                    count_tri<COUNT, DIAG>(cnt);
+                    if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+                }
+            }
+        }
+#endif
+        for (; off < offEnd; off += kPairRecordBytes) {
+            const PairHit ph = rayTrianglePair(ray, load_pair_at(pbase, off));
+#if WCPT_DUP_PAIR
+            {
+                Ray r2 = ray;
+                r2.origin.x = launder(r2.origin.x);
+                const PairHit p2 = rayTrianglePair(r2, load_pair_at(pbase, off));
+                sink(p2.t.x + p2.t.y);
+                sink_u((p2.hit0 ? 1u : 0u) | (p2.hit1 ? 2u : 0u));
+            }
+#endif
+            count_tri<COUNT, DIAG>(cnt);
+            if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
+            count_tri<COUNT, DIAG>(cnt);
+            if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+        }
+        if (tag != kNoTag) prim = 3u * (2u * (tag / kPairRecordBytes) + (tag & 1u));
+        if (k < kfull) k = kfull;
+        if (k < kend) {
+            const PairHit ph = rayTrianglePair(ray, load_pair(g.tris, k >> 1));
+            count_tri<COUNT, DIAG>(cnt);
+            if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
+        }
+    } else {
+        for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
+            const uint32_t first = k + curLeft;
+            const TriE tr = (!PAIRS && k0 != kNoRecord) ? load_tri(g.tris, k0 + j)
+                                                        : tri_from_indices(g.indices, g.vertices, first);
+            const float t = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
+            count_tri<COUNT, DIAG>(cnt);
+            if (t != -1.0f && t < rt) {
+                rt = t;
+                prim = first;
+            }
+        }
+    }
+    phase_mark(cnt, 3);
+}
+
+/* Interior (:179-199): fetch both children (64 contiguous bytes), test both boxes, push the farther child if it
+ * passes, and return true with the cursor on the nearer child if that one passes and is not culled by rec.t. */
+template <bool COUNT, bool DIAG, class Stack>
+__device__ __forceinline__ bool interior_step(const Ray& ray, const DrawGeom& g, Stack& stk, uint32_t& curLeft,
+                                              uint32_t& curCount, float rt, Counters& cnt, bool& overflow)
+{
+    const NodeV L = load_node(g.bvh, curLeft);
+    const NodeV R = load_node(g.bvh, curLeft + 1);
+    float l0, l1, r0, r1;
+    node_box(ray, L, l0, l1);
+    node_box(ray, R, r0, r1);
+#if WCPT_DUP_BOX
+    {
+        Ray r2 = ray;
+        r2.origin.x = launder(r2.origin.x);
+        r2.origin.y = launder(r2.origin.y);
+        r2.origin.z = launder(r2.origin.z);
+        float a0, a1, b0, b1;
+        node_box(r2, L, a0, a1);
+        node_box(r2, R, b0, b1);
+        sink(a0 + a1 + b0 + b1);
+    }
+#endif
+    if (COUNT) {
+        cnt.interior_visits++;
+        cnt.node_pops += 2;
+        simd_step<DIAG>(cnt.wave_int, cnt.lane_int);
+    }
+    const float leftDist = (l0 > 0.0f) ? l0 : l1;
+    const float rightDist = (r0 > 0.0f) ? r0 : r1;
+    const bool passL = !(l0 > l1 || l1 < 0.0f);
+    const bool passR = !(r0 > r1 || r1 < 0.0f);
+    /* reference order: left popped first iff leftDist < rightDist */
+    const bool leftFirst = leftDist < rightDist;
+    const uint32_t farIdx = leftFirst ? curLeft + 1 : curLeft;
+    const bool passNear = leftFirst ? passL : passR;
+    const bool passFar = leftFirst ? passR : passL;
+    const float nearT0 = leftFirst ? l0 : r0;
+    const float farT0 = leftFirst ? r0 : l0;
+    const NodeV& F = leftFirst ? R : L;
+    if (passFar && !stk.push(node_ref(g.packed, farIdx, F.b.z, F.b.w), farT0)) overflow = true;
+    phase_mark(cnt, 2);
+    if (passNear && !(nearT0 > rt)) {
+        const NodeV& N = leftFirst ? L : R;
+        curLeft = N.b.z;
+        curCount = N.b.w;
+        return true;
+    }
+    return false;
+}
+
+/* Pop (:157-162): the next deferred node whose box entry distance is not beyond rec.t; false when none is left. */
+template <class Stack>
+__device__ __forceinline__ bool pop_step(const DrawGeom& g, Stack& stk, uint32_t& curLeft, uint32_t& curCount, float rt,
+                                         Counters& cnt)
+{
+    bool found = false;
+    while (!stk.empty()) {
+        uint32_t ni;
+        float t0;
+        stk.pop(ni, t0);
+        if (t0 > rt) continue;
+        const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
+        curLeft = lc.x;
+        curCount = lc.y;
+        found = true;
+        break;
+    }
+    phase_mark(cnt, 2);
+    return found;
+}
+
+/* The root of draw d (:152-162): pushed untested, popped and tested. Returns true with the cursor on the root when it
+ * survives the cull. */
+template <bool COUNT>
+__device__ __forceinline__ bool root_step(const Ray& ray, const DrawGeom& g, float rt, uint32_t& curLeft,
+                                          uint32_t& curCount, Counters& cnt)
+{
+    if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
+    const NodeV cur = load_node(g.bvh, 0);
+    float c0, c1;
+    node_box(ray, cur, c0, c1);
+    if (c0 > c1 || c1 < 0.0f || c0 > rt) return false;
+    curLeft = cur.b.z;
+    curCount = cur.b.w;
+    return true;
+}
+
+/* pathTracer.comp:135-211. PAIRS: leaf tests on pair records (else single records).
+ *
+ * SINGLE (drawCommandCount == 1, the reference's own case, PathTracingRenderer.jai:251): the draw's geometry is
+ * kernel-uniform and its traversal runs once, without the draw loop. Otherwise the draws are walked inside the one
+ * traversal loop (the next draw starts when the stack of the current one is exhausted), like wf_trace: the nested
+ * form -- a loop over draws containing the divergent traversal loops, inside the divergent bounce loop -- is
+ * mis-compiled by this toolchain whenever the traversal grows (a DIAG build or the scalar-load leaf loop on the
+ * atrium overflowed the stack, tools/stack_probe.py), while this flat form is not. */
+template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
                                          const wcpt_draw_command* __restrict__ draws,
                                          const uint64_t* __restrict__ tri_records, Stack& stk,
@@ -819,160 +1045,74 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
 #endif
     phase_mark(cnt, 1);
 
-    for (uint32_t i = 0; i < sd.drawCommandCount; i++) {
-        const gnode_ptr bvh = as_nodes(draws[i].bvhBuffer);
-        const gu32_ptr indices = as_u32(draws[i].indexBuffer);
-        const gf32_ptr vertices = as_f32(draws[i].vertexBuffer);
-        const gtri_ptr tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + (PAIRS ? 1u : 0u)];
-        const uint32_t ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
-        const bool packed = (tri_records[kTriTableWords * i + 3u] & kTriFlagPackedRefs) != 0u;
-        if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
-        const float rt_before = rt; /* a hit in this draw lowers rt (strict <): then it owns prim */
-
-        /* root: pushed untested, popped and tested (:155-162) */
-        NodeV cur = load_node(bvh, 0);
-        float c0, c1;
-        node_box(ray, cur, c0, c1);
-        if (c0 > c1 || c1 < 0.0f || c0 > rt) continue;
-        uint32_t curLeft = cur.b.z, curCount = cur.b.w;
-        stk.reset();
-        for (;;) {
-            if (curCount > 0) {
-                /* leaf (:164-178) */
-                const uint32_t k0 = leaf_record(curLeft, curCount, ntri);
-                if (PAIRS && k0 != kNoRecord) {
-                    /* triangles [k0, kend) in pair records (2j, 2j+1): a leaf that starts in the second slot of
-                     * a pair tests that pair for its first triangle, then whole pairs, then possibly the first
-                     * slot of a last pair -- no per-iteration slot checks; applied in index order, strict < */
-                    const uint32_t kend = k0 + (curCount + 2u) / 3u;
-                    uint32_t k = k0;
-                    if (k & 1u) {
-                        const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
-                        count_tri<COUNT, DIAG>(cnt);
-                        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
-                        k++;
-                    }
-#if WCPT_PAIR_OFFSET_LOOP
-                    /* whole pairs: one 32-bit byte-offset induction variable from the draw's (uniform) record base
-                     * (global_load with an SGPR base), and the winner recorded as a tag -- the pair's offset for its
-                     * first triangle, offset + 1 for its second -- decoded into the index position once per leaf */
-                    {
-                        const uint32_t kfull = kend & ~1u;
-                        const WCPT_GLOBAL char* pbase = reinterpret_cast<const WCPT_GLOBAL char*>(tris);
-                        const uint32_t offEnd = (kfull >> 1) * kPairRecordBytes;
-                        uint32_t off = (k >> 1) * kPairRecordBytes, tag = kNoTag;
-                        for (; off < offEnd; off += kPairRecordBytes) {
-                            const PairHit ph = rayTrianglePair(ray, load_pair_at(pbase, off));
-#if WCPT_DUP_PAIR
-                            {
-                                Ray r2 = ray;
-                                r2.origin.x = launder(r2.origin.x);
-                                const PairHit p2 = rayTrianglePair(r2, load_pair_at(pbase, off));
-                                sink(p2.t.x + p2.t.y);
-                                sink_u((p2.hit0 ? 1u : 0u) | (p2.hit1 ? 2u : 0u));
-                            }
+    uint32_t curLeft = 0, curCount = 0;
+    if constexpr (SINGLE) {
+        const DrawGeom g = draw_geom<PAIRS>(draws, tri_records, 0);
+#ifndef WCPT_MK_FLAT
+#define WCPT_MK_FLAT 1
 #endif
-                            count_tri<COUNT, DIAG>(cnt);
-                            if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
-                            count_tri<COUNT, DIAG>(cnt);
-                            if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
-                        }
-                        if (tag != kNoTag) prim = 3u * (2u * (tag / kPairRecordBytes) + (tag & 1u));
-                        if (k < kfull) k = kfull;
-                    }
+#if WCPT_MK_FLAT
+        /* one traversal step per iteration as sequential ifs on the lane's mode (pop -> interior -> leaf), like
+         * wf_trace: a lane that pops an interior node visits it in the same iteration, one that descends into a
+         * leaf tests it in the same iteration */
+        enum : uint32_t { kInterior = 0, kLeaf = 1, kPop = 2, kDone = 3 };
+        uint32_t mode = kDone;
+        if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
+            stk.reset();
+            mode = curCount > 0 ? kLeaf : kInterior;
+        }
+        while (mode != kDone) {
+            if (mode == kPop)
+                mode = pop_step(g, stk, curLeft, curCount, rt, cnt) ? (curCount > 0 ? kLeaf : kInterior) : kDone;
+            if (mode == kInterior)
+                mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)
+                           ? (curCount > 0 ? kLeaf : kInterior) : kPop;
+            if (mode == kLeaf) {
+                leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt);
+                mode = kPop;
+            }
+        }
 #else
-                    for (const uint32_t kfull = kend & ~1u; k < kfull; k += 2) {
-                        const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
-                        count_tri<COUNT, DIAG>(cnt);
-                        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
-                        count_tri<COUNT, DIAG>(cnt);
-                        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * (k + 1u); }
-                    }
-#endif
-                    if (k < kend) {
-                        const PairHit ph = rayTrianglePair(ray, load_pair(tris, k >> 1));
-                        count_tri<COUNT, DIAG>(cnt);
-                        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
-                    }
-                } else {
-                    for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
-                        const uint32_t first = k + curLeft;
-                        const TriE tr = (!PAIRS && k0 != kNoRecord) ? load_tri(tris, k0 + j)
-                                                                    : tri_from_indices(indices, vertices, first);
-                        const float t = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
-                        if (COUNT) {
-                            cnt.triangle_tests++;
-                            simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
-                        }
-                        if (t != -1.0f && t < rt) {
-                            rt = t;
-                            prim = first;
-                        }
-                    }
-                }
-                phase_mark(cnt, 3);
-            } else {
-                /* interior (:179-199): fetch both children (64 contiguous bytes), test both boxes */
-                const NodeV L = load_node(bvh, curLeft);
-                const NodeV R = load_node(bvh, curLeft + 1);
-                float l0, l1, r0, r1;
-                node_box(ray, L, l0, l1);
-                node_box(ray, R, r0, r1);
-#if WCPT_DUP_BOX
-                {
-                    Ray r2 = ray;
-                    r2.origin.x = launder(r2.origin.x);
-                    r2.origin.y = launder(r2.origin.y);
-                    r2.origin.z = launder(r2.origin.z);
-                    float a0, a1, b0, b1;
-                    node_box(r2, L, a0, a1);
-                    node_box(r2, R, b0, b1);
-                    sink(a0 + a1 + b0 + b1);
-                }
-#endif
-                if (COUNT) {
-                    cnt.interior_visits++;
-                    cnt.node_pops += 2;
-                    simd_step<DIAG>(cnt.wave_int, cnt.lane_int);
-                }
-                const float leftDist = (l0 > 0.0f) ? l0 : l1;
-                const float rightDist = (r0 > 0.0f) ? r0 : r1;
-                const bool passL = !(l0 > l1 || l1 < 0.0f);
-                const bool passR = !(r0 > r1 || r1 < 0.0f);
-                /* reference order: left popped first iff leftDist < rightDist */
-                const bool leftFirst = leftDist < rightDist;
-                const uint32_t farIdx = leftFirst ? curLeft + 1 : curLeft;
-                const bool passNear = leftFirst ? passL : passR;
-                const bool passFar = leftFirst ? passR : passL;
-                const float nearT0 = leftFirst ? l0 : r0;
-                const float farT0 = leftFirst ? r0 : l0;
-                const NodeV& F = leftFirst ? R : L;
-                if (passFar && !stk.push(node_ref(packed, farIdx, F.b.z, F.b.w), farT0)) overflow = true;
-                if (passNear && !(nearT0 > rt)) {
-                    const NodeV& N = leftFirst ? L : R;
-                    curLeft = N.b.z;
-                    curCount = N.b.w;
-                    phase_mark(cnt, 2);
+        if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
+            stk.reset();
+            for (;;) {
+                if (curCount > 0) {
+                    leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt);
+                } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)) {
                     continue;
                 }
+                if (!pop_step(g, stk, curLeft, curCount, rt, cnt)) break;
             }
-            /* pop (:157-162) */
-            bool found = false;
-            while (!stk.empty()) {
-                uint32_t ni;
-                float t0;
-                stk.pop(ni, t0);
-                if (t0 > rt) continue;
-                const uint2 lc = node_ref_lc(packed, bvh, ni);
-                curLeft = lc.x;
-                curCount = lc.y;
-                found = true;
-                break;
-            }
-            phase_mark(cnt, 2);
-            if (!found) break;
         }
-        if (rt != rt_before) primDraw = i;
+#endif
+    } else {
+        uint32_t d = 0;
+        DrawGeom g;
+        float rt_before = rt;
+        /* first draw (from d on) whose root survives the cull */
+        auto start_draw = [&]() {
+            for (; d < sd.drawCommandCount; d++) {
+                g = draw_geom<PAIRS>(draws, tri_records, d);
+                rt_before = rt;
+                if (root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
+                    stk.reset();
+                    return true;
+                }
+            }
+            return false;
+        };
+        bool active = start_draw();
+        while (active) {
+            if (curCount > 0) {
+                leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt);
+            } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)) {
+                continue;
+            }
+            if (pop_step(g, stk, curLeft, curCount, rt, cnt)) continue;
+            if (rt != rt_before) primDraw = d; /* this draw lowered rt: it owns prim */
+            d++;
+            active = start_draw();
+        }
     }
 
     if (COUNT && prim != kNoPrim) cnt.hits++;
@@ -1122,7 +1262,7 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
 }
 
 /* pathTracer.comp:241-284 */
-template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
+template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
 __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_data& sd,
                                        const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
                                        const wcpt_draw_command* __restrict__ draws,
@@ -1133,7 +1273,7 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
     path_begin(ps, ray.origin, ray.direction);
     f3 L;
     for (;;) {
-        const Hit h = intersect<COUNT, DIAG, PAIRS>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
+        const Hit h = intersect<COUNT, DIAG, PAIRS, SINGLE>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
         const bool done = path_shade(ps, h, rng, sd, mats, L);
         phase_mark(cnt, 5);
         if (done) return L;

@@ -40,7 +40,7 @@ __device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTot
 }
 
 /* Shade one pixel (pathTracer.comp:290-323) with the given traversal stack. */
-template <bool COUNT, bool DIAG, bool PAIRS, class Stack>
+template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
 __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcpt_material* __restrict__ mats,
                                             const wcpt_sphere* __restrict__ spheres,
                                             const wcpt_draw_command* __restrict__ draws,
@@ -66,7 +66,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
         r.origin = origin;
         r.direction = dir;
         r.invDirection = rcp3(dir);
-        result = result + TraceRay<COUNT, DIAG, PAIRS>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow);
+        result = result + TraceRay<COUNT, DIAG, PAIRS, SINGLE>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow);
     }
     result = result / (float)sd.samples; /* :312 */
     if (!COUNT) {
@@ -91,7 +91,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
 #ifndef WCPT_MK_WAVES
 #define WCPT_MK_WAVES 1
 #endif
-template <bool COUNT, bool DIAG, int SK, bool PAIRS>
+template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE>
 __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                     const wcpt_sphere* __restrict__ spheres,
                                                     const wcpt_draw_command* __restrict__ draws,
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
             uint64_t mem[kPrivateStack];
             PrivateStack<kPrivateStack> stk;
             stk.mem = (priv_u64_ptr)mem;
-            shade_pixel<COUNT, DIAG, PAIRS>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
+            shade_pixel<COUNT, DIAG, PAIRS, SINGLE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
                                             cnt, overflow);
         } else {
             __shared__ uint64_t s_stack[kLdsStack * 64];
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
             LdsStack<kLdsStack, kSpillStack> stk;
             stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
             stk.spill = (priv_u64_ptr)spill;
-            shade_pixel<COUNT, DIAG, PAIRS>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
+            shade_pixel<COUNT, DIAG, PAIRS, SINGLE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
                                             cnt, overflow);
         }
     }
@@ -298,7 +298,7 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
     return hipGetLastError();
 }
 
-template <bool COUNT, bool DIAG, int SK, bool PAIRS>
+template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE>
 static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
 {
     /* scattered tile order: block b renders tile (b * m) mod tiles for an m coprime with tiles near 0.618 * tiles,
@@ -311,24 +311,24 @@ static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stre
         while (gcd(m, tiles) != 1u) m += 2u;
         scatter = m;
     }
-    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS>), dim3(tiles), dim3(64), 0, stream, a.sd,
+    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE>), dim3(tiles), dim3(64), 0, stream, a.sd,
                        a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H, a.y0,
                        a.rows, tilesX, tiles, scatter, a.status, a.counters);
     return hipGetLastError();
 }
 
-template <bool PAIRS>
+template <bool PAIRS, bool SINGLE>
 static hipError_t launch_mega_sk(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream,
                                  uint32_t tilesX, uint32_t tiles)
 {
     if (stack_kind == 0) {
-        if (mode == kModeRender) return launch_mega<false, false, 0, PAIRS>(a, mk, stream, tilesX, tiles);
-        if (mode == kModeCount) return launch_mega<true, false, 0, PAIRS>(a, mk, stream, tilesX, tiles);
-        return launch_mega<true, true, 0, PAIRS>(a, mk, stream, tilesX, tiles);
+        if (mode == kModeRender) return launch_mega<false, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+        if (mode == kModeCount) return launch_mega<true, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+        return launch_mega<true, true, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
     }
-    if (mode == kModeRender) return launch_mega<false, false, 1, PAIRS>(a, mk, stream, tilesX, tiles);
-    if (mode == kModeCount) return launch_mega<true, false, 1, PAIRS>(a, mk, stream, tilesX, tiles);
-    return launch_mega<true, true, 1, PAIRS>(a, mk, stream, tilesX, tiles);
+    if (mode == kModeRender) return launch_mega<false, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+    if (mode == kModeCount) return launch_mega<true, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+    return launch_mega<true, true, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
 }
 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream)
@@ -343,8 +343,14 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
         if (e == hipSuccess) e = hipDeviceGetAttribute(&mk.cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
     }
-    if (a.pair_records) return launch_mega_sk<true>(a, mode, stack_kind, mk, stream, tilesX, tiles);
-    return launch_mega_sk<false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    /* one draw command (the reference's case): the single-draw instantiation, without the draw loop */
+    const bool single = a.sd.drawCommandCount == 1u;
+    if (a.pair_records) {
+        if (single) return launch_mega_sk<true, true>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+        return launch_mega_sk<true, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    }
+    if (single) return launch_mega_sk<false, true>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    return launch_mega_sk<false, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
 }
 
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n, hipStream_t stream)
