@@ -1048,10 +1048,6 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     uint32_t curLeft = 0, curCount = 0;
     if constexpr (SINGLE) {
         const DrawGeom g = draw_geom<PAIRS>(draws, tri_records, 0);
-#ifndef WCPT_MK_FLAT
-#define WCPT_MK_FLAT 1
-#endif
-#if WCPT_MK_FLAT
         /* one traversal step per iteration as sequential ifs on the lane's mode (pop -> interior -> leaf), like
          * wf_trace: a lane that pops an interior node visits it in the same iteration, one that descends into a
          * leaf tests it in the same iteration */
@@ -1072,19 +1068,6 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 mode = kPop;
             }
         }
-#else
-        if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
-            stk.reset();
-            for (;;) {
-                if (curCount > 0) {
-                    leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt);
-                } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)) {
-                    continue;
-                }
-                if (!pop_step(g, stk, curLeft, curCount, rt, cnt)) break;
-            }
-        }
-#endif
     } else {
         uint32_t d = 0;
         DrawGeom g;
