@@ -103,13 +103,18 @@ def main():
             for f in range(args.warmup):
                 step(f, gather)
             torch.cuda.synchronize()
-            ctx.profile_begin()
             t0 = time.perf_counter()
             for k in range(args.steps):
                 step(args.warmup + k, gather)
             t_host = time.perf_counter() - t0
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
+            # kernel time in a separate pass, as bench.py at N > 1 (per-launch events are kept out of timed steps)
+            ctx.set_gather_output(0, 0)
+            ctx.profile_begin()
+            for k in range(args.steps):
+                sd["renderedFramesCount"] = args.warmup + k
+                ctx.render(sd, *addrs)
             kms, launches = ctx.profile_end()
             res[gather] = (el / args.steps * 1e3, t_host / args.steps * 1e3, kms / max(1, launches))
         print(f"N={n} rows={rows}: render-only {res[False][0]:.4f} ms/step (host {res[False][1]:.4f}), "
