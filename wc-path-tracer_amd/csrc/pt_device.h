@@ -488,6 +488,9 @@ constexpr uint32_t kNoTag = 0xFFFFFFFFu;
 #ifndef WCPT_PAIR_UNIFORM
 #define WCPT_PAIR_UNIFORM 1
 #endif
+#ifndef WCPT_PAIR_SLOOP
+#define WCPT_PAIR_SLOOP 1
+#endif
 
 __device__ __forceinline__ TriPair load_pair_at(const WCPT_GLOBAL char* base, uint32_t off)
 {
@@ -867,6 +870,19 @@ __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uin
             uint32_t diff = (off ^ offU) | (offEnd ^ endU);
             asm volatile("" : "+v"(diff));
             if (diff == 0u) {
+#if WCPT_PAIR_SLOOP
+                /* the loop counter itself in an SGPR (offU..endU): no per-lane offset arithmetic (70 -> 68 VALU per
+                 * pair, c2 -1.7 %). A wave-uniform loop like this one was mis-compiled inside the old nested draw
+                 * loop; in the flat traversal loop it is correct (tools/stack_probe.py) */
+                for (uint32_t o = offU; o < endU; o += kPairRecordBytes) {
+                    const PairHit ph = rayTrianglePair(ray, load_pair_const(pbase, o));
+                    count_tri<COUNT, DIAG>(cnt);
+                    if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = o; }
+                    count_tri<COUNT, DIAG>(cnt);
+                    if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = o + 1u; }
+                }
+                off = offEnd;
+#else
                 for (; off < offEnd; off += kPairRecordBytes) {
                     const PairHit ph = rayTrianglePair(ray, load_pair_const(pbase, __builtin_amdgcn_readfirstlane(off)));
                     count_tri<COUNT, DIAG>(cnt);
@@ -874,6 +890,7 @@ __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uin
                     count_tri<COUNT, DIAG>(cnt);
                     if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
                 }
+#endif
             }
         }
 #endif
