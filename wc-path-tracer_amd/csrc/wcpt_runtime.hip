@@ -131,7 +131,10 @@ struct wcpt_context {
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (c3: 12 -> 6.83 ms, 20..32 -> 6.73, 48 -> 7.03) */
-    int wf_pipes = 2;                  /* WCPT_OPTION_WF_PIPES (2: c3 -2%, a c4 8-way row block -10%) */
+#ifndef WCPT_WF_PIPES_DEFAULT
+#define WCPT_WF_PIPES_DEFAULT 2
+#endif
+    int wf_pipes = WCPT_WF_PIPES_DEFAULT; /* WCPT_OPTION_WF_PIPES (2: c3 -2%, a c4 8-way row block -10%) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
