@@ -359,6 +359,9 @@ constexpr uint32_t kNoPrim = 0xFFFFFFFFu, kSpherePrim = 0x80000000u;
 #ifndef WCPT_SPHERE_PAIRS
 #define WCPT_SPHERE_PAIRS 1
 #endif
+#ifndef WCPT_SPHERE_BSKIP
+#define WCPT_SPHERE_BSKIP 1
+#endif
 __device__ __forceinline__ void sphere_loop(const Ray& r, uint32_t count, const wcpt_sphere* __restrict__ spheres,
                                             float& rt, uint32_t& prim)
 {
@@ -376,8 +379,15 @@ __device__ __forceinline__ void sphere_loop(const Ray& r, uint32_t count, const 
         const v2f b = (ocx * dx + ocy * dy) + ocz * dz;           /* dot(oc, d) */
         const v2f c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - rad * rad;
         const v2f t = b * b - c;
+#if WCPT_SPHERE_BSKIP
+        /* b >= 0 (the centre is not ahead of the origin) gives -b - sqrt(t) <= 0 exactly, so RN of it is <= 0 and the
+         * `t0 > 0` test below fails either way: the square root is skipped (NaN b still takes the full path) */
+        const float t0 = (t.x < 0.0f || b.x >= 0.0f) ? -1.0f : -b.x - sqrt_exact(t.x);
+        const float t1 = (t.y < 0.0f || b.y >= 0.0f) ? -1.0f : -b.y - sqrt_exact(t.y);
+#else
         const float t0 = t.x < 0.0f ? -1.0f : -b.x - sqrt_exact(t.x);
         const float t1 = t.y < 0.0f ? -1.0f : -b.y - sqrt_exact(t.y);
+#endif
         if (t0 > 0.0f && t0 < rt) { rt = t0; prim = kSpherePrim | i; }
         if (t1 > 0.0f && t1 < rt) { rt = t1; prim = kSpherePrim | (i + 1u); }
     }
