@@ -868,11 +868,9 @@ __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uin
 #if WCPT_PAIR_UNIFORM
         if (UNIFORM) {
             /* Lanes whose whole-pair range equals the first active lane's (in a coherent wave: all of them) read
-             * the records at that lane's offset with scalar loads: the offset is re-derived each iteration with
-             * readfirstlane, so the loads are wave-uniform, go through the scalar cache (no per-lane addresses, no
-             * vector-memory return of 64 copies of the record) and the packed-FP32 instructions take the record
-             * straight from SGPRs (c2 -8%). The loop stays an ordinary per-lane loop. The other lanes take the
-             * per-lane loop below. */
+             * the records at wave-uniform offsets with scalar loads: they go through the scalar cache (no per-lane
+             * addresses, no vector-memory return of 64 copies of the record) and the packed-FP32 instructions take
+             * the record straight from SGPRs (c2 -6 %). The other lanes take the per-lane loop below. */
             const uint32_t offU = __builtin_amdgcn_readfirstlane(off);
             const uint32_t endU = __builtin_amdgcn_readfirstlane(offEnd);
             /* tested through an opaque value: a plain `off == offU` lets the compiler substitute the equal
@@ -893,6 +891,7 @@ __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uin
                 }
                 off = offEnd;
 #else
+                /* per-lane loop counter, offset re-derived with readfirstlane each iteration */
                 for (; off < offEnd; off += kPairRecordBytes) {
                     const PairHit ph = rayTrianglePair(ray, load_pair_const(pbase, __builtin_amdgcn_readfirstlane(off)));
                     count_tri<COUNT, DIAG>(cnt);
