@@ -442,6 +442,42 @@ def test_multi_draw_deep_trees_match_oracle(gpu_ctx, kernel, pairs, combo):
     assert cnt == rcnt
 
 
+def test_primary_records_follow_the_camera(gpu_ctx):
+    """The megakernel tests a sample's first segment against primary-ray pair records derived for the camera
+    position (pt_device.h TriPairP). They are cached per position: moving the camera between frames of one context,
+    moving it back, and re-uploading the mesh at a fixed camera must each give the oracle's frame (2 spp: every
+    sample's first segment starts at the camera)."""
+    import copy
+    import ctypes
+    s = get_scene("cornell")
+    W, H = 48, 40
+    cams = []
+    for dx in (0.0, 0.35, 0.0):
+        cam = wcpt.Camera()
+        ctypes.pointer(cam)[0] = s.camera
+        cam.position[0] += dx
+        cam.position[1] += dx * 0.5
+        cams.append(cam)
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+    gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, 1)
+    try:
+        gpu_ctx.create_screen(W, H)
+        for f, cam in enumerate(cams + [cams[-1]]):
+            if f == 3:  # same camera, mesh re-uploaded: the pair records are rebuilt, the primary records follow
+                m = s.meshes[0]
+                gpu_ctx.buffer_upload(dev.buffers[2], np.ascontiguousarray(m.positions, dtype=np.float32))
+            sd = s.scene_data(W, H, max_bounce=3, samples=2, frame=0, camera=cam)
+            gpu_ctx.render(sd, *dev.addresses())
+            gpu_ctx.sync()
+            img = gpu_ctx.readback()
+            ref, _ = oracle.render_scene(copy.copy(s), W, H, sd=sd, threads=8)
+            assert_close(img, ref)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, -1)
+        dev.free()
+
+
 @pytest.mark.parametrize("pairs", [0, 1])
 @pytest.mark.parametrize("stack", [0, 1])
 def test_megakernel_atrium_rows_all_modes(gpu_ctx, pairs, stack):

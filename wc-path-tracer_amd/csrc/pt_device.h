@@ -462,8 +462,9 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { r
  * The reference's BVH keeps each leaf's index triples contiguous (PathTracingRenderer.jai:233), so a leaf's
  * records are contiguous. A leaf whose first index position is not a multiple of 3 (never produced by the
  * reference's builder) or that reaches past the draw's indexCount uses the index path.
- * Per-draw table entry: {single record address, pair record address, triangle count, flags} (4 x u64). */
-constexpr uint32_t kTriTableWords = 4;
+ * Per-draw table entry: {single record address, pair record address, triangle count, flags, primary-ray pair record
+ * address or 0} (5 x u64). */
+constexpr uint32_t kTriTableWords = 5;
 constexpr uint64_t kTriFlagPackedRefs = 1u; /* table word 3: stack entries may carry (left, count) */
 constexpr uint64_t kTriFlagIndex24 = 2u;    /* table word 3: the draw's indexCount is < 2^24 */
 typedef const WCPT_GLOBAL v4f* gtri_ptr;
@@ -565,6 +566,79 @@ __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& 
 #endif
     return h;
 }
+/* Primary-ray pair records. Every primary ray of a frame starts at the camera (pathTracer.comp:299-302, SceneData
+ * position), so the terms of rayTrianglePair that depend only on the origin and the triangle -- oa = o - a, q =
+ * cross(oa, e1) and the t numerator dot(e2, q) (:124-125, :127, :130) -- are the same for every primary ray. The
+ * runtime derives them once per camera position (build_primary_pairs, the same binary32 operations in the same
+ * order, so the values are bit-identical) and the first segment of each sample tests its leaves from these records:
+ * 51 instead of 68 VALU per pair. 112 B per pair: (e1x, e1y) (e1z, e2x) (e2y, e2z) (oax, oay) (oaz, qx) (qy, qz)
+ * (tq, pad), each a float2 {triangle 2j, 2j+1}. */
+#ifndef WCPT_PRIMARY_PAIRS
+#define WCPT_PRIMARY_PAIRS 1
+#endif
+constexpr uint32_t kPrimPairFloat4s = 7;
+constexpr uint32_t kPrimPairRecordBytes = 16u * kPrimPairFloat4s;
+struct TriPairP { v2f e1x, e1y, e1z, e2x, e2y, e2z, oax, oay, oaz, qx, qy, qz, tq; };
+template <class P>
+__device__ __forceinline__ TriPairP unpack_pairP(P q)
+{
+    const v4f r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4], r5 = q[5], r6 = q[6];
+    TriPairP p;
+    p.e1x = r0.xy; p.e1y = r0.zw;
+    p.e1z = r1.xy; p.e2x = r1.zw;
+    p.e2y = r2.xy; p.e2z = r2.zw;
+    p.oax = r3.xy; p.oay = r3.zw;
+    p.oaz = r4.xy; p.qx = r4.zw;
+    p.qy = r5.xy;  p.qz = r5.zw;
+    p.tq = r6.xy;
+    return p;
+}
+__device__ __forceinline__ TriPairP load_pairP_at(const WCPT_GLOBAL char* base, uint32_t off)
+{
+    return unpack_pairP(reinterpret_cast<gtri_ptr>(base + off));
+}
+__device__ __forceinline__ TriPairP load_pairP_const(const WCPT_GLOBAL char* base, uint32_t off)
+{
+    return unpack_pairP((ctri_ptr)(uintptr_t)(base + off));
+}
+/* rayTrianglePair with the origin terms taken from the record: the remaining operations are rayTrianglePair's */
+__device__ __forceinline__ PairHit rayTrianglePairP(const Ray& r, const TriPairP& p)
+{
+    const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
+    const v2f px = dy * p.e2z - p.e2y * dz;
+    const v2f py = dz * p.e2x - p.e2z * dx;
+    const v2f pz = dx * p.e2y - p.e2x * dy;
+    const v2f det = (p.e1x * px + p.e1y * py) + p.e1z * pz;
+    const v2f inv = rcp2_exact(det);
+    const v2f u = ((p.oax * px + p.oay * py) + p.oaz * pz) * inv;
+    const v2f v = (dx * (p.qx * inv) + dy * (p.qy * inv)) + dz * (p.qz * inv);
+    const v2f t = p.tq * inv;
+    const v2f uv = u + v;
+    PairHit h;
+    h.t = t;
+#if WCPT_ACCEPT_MIN3
+    const v2f w = bc2(1.0f) - uv;
+    h.hit0 = accept_tri_w(t.x, u.x, v.x, w.x);
+    h.hit1 = accept_tri_w(t.y, u.y, v.y, w.y);
+#else
+    h.hit0 = accept_tri(t.x, u.x, v.x, uv.x);
+    h.hit1 = accept_tri(t.y, u.y, v.y, uv.y);
+#endif
+    return h;
+}
+/* The origin terms of one triangle (half h of pair record q) for origin o: build_primary_pairs */
+__device__ __forceinline__ void primary_terms(float ox, float oy, float oz, float ax, float ay, float az, float e1x,
+                                              float e1y, float e1z, float e2x, float e2y, float e2z, float out[7])
+{
+    const float oax = ox - ax, oay = oy - ay, oaz = oz - az;
+    const float qx = oay * e1z - e1y * oaz;
+    const float qy = oaz * e1x - e1z * oax;
+    const float qz = oax * e1y - e1x * oay;
+    out[0] = oax; out[1] = oay; out[2] = oaz;
+    out[3] = qx;  out[4] = qy;  out[5] = qz;
+    out[6] = (e2x * qx + e2y * qy) + e2z * qz;
+}
+
 __device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
 {
     const f3 a = ld3(vtx + 3ull * idx[first + 0]);
@@ -820,7 +894,8 @@ struct DrawGeom {
     gnode_ptr bvh;
     gu32_ptr indices;
     gf32_ptr vertices;
-    gtri_ptr tris; /* pair records (PAIRS) or single records */
+    gtri_ptr tris;  /* pair records (PAIRS) or single records */
+    gtri_ptr ptris; /* primary-ray pair records (PAIRS, when the runtime built them; table word 4) or null */
     uint32_t ntri;
     bool packed; /* stack entries carry (left, count): kTriFlagPackedRefs */
 };
@@ -833,99 +908,111 @@ __device__ __forceinline__ DrawGeom draw_geom(const wcpt_draw_command* __restric
     g.indices = as_u32(draws[i].indexBuffer);
     g.vertices = as_f32(draws[i].vertexBuffer);
     g.tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + (PAIRS ? 1u : 0u)];
+    g.ptris = PAIRS ? (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + 4u] : nullptr;
     g.ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
     g.packed = (tri_records[kTriTableWords * i + 3u] & kTriFlagPackedRefs) != 0u;
     return g;
 }
 
+/* The pair-record part of a leaf (:164-178): triangles [k0, kend) in pair records (2j, 2j+1), from `recs` (pair
+ * records, or primary-ray pair records when PRIM). A leaf that starts in the second slot of a pair tests that pair
+ * for its first triangle, then whole pairs, then possibly the first slot of a last pair -- no per-iteration slot
+ * checks; applied in index order, strict <. UNIFORM: lanes of a coherent wave walk the whole pairs with scalar loads
+ * (the record base must be wave-uniform). */
+template <bool COUNT, bool DIAG, bool UNIFORM, bool PRIM>
+__device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_t k0, uint32_t kend, float& rt,
+                                          uint32_t& prim, Counters& cnt)
+{
+    constexpr uint32_t kBytes = PRIM ? kPrimPairRecordBytes : kPairRecordBytes;
+    const WCPT_GLOBAL char* pbase = reinterpret_cast<const WCPT_GLOBAL char*>(recs);
+    auto test_at = [&](uint32_t off) {
+        if constexpr (PRIM) return rayTrianglePairP(ray, load_pairP_at(pbase, off));
+        else return rayTrianglePair(ray, load_pair_at(pbase, off));
+    };
+    uint32_t k = k0;
+    if (k & 1u) {
+        const PairHit ph = test_at((k >> 1) * kBytes);
+        count_tri<COUNT, DIAG>(cnt);
+        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
+        k++;
+    }
+    /* whole pairs: one 32-bit byte-offset induction variable from the draw's record base, and the winner recorded
+     * as a tag -- the pair's offset for its first triangle, offset + 1 for its second -- decoded into the index
+     * position once per leaf */
+    const uint32_t kfull = kend & ~1u;
+    const uint32_t offEnd = (kfull >> 1) * kBytes;
+    uint32_t off = (k >> 1) * kBytes, tag = kNoTag;
+#if WCPT_PAIR_UNIFORM
+    if (UNIFORM) {
+        /* Lanes whose whole-pair range equals the first active lane's (in a coherent wave: all of them) read the
+         * records at wave-uniform offsets with scalar loads: they go through the scalar cache (no per-lane
+         * addresses, no vector-memory return of 64 copies of the record) and the packed-FP32 instructions take the
+         * record straight from SGPRs (c2 -6 %). The other lanes take the per-lane loop below. */
+        const uint32_t offU = __builtin_amdgcn_readfirstlane(off);
+        const uint32_t endU = __builtin_amdgcn_readfirstlane(offEnd);
+        /* tested through an opaque value: a plain `off == offU` lets the compiler substitute the equal per-lane
+         * value back into the loads */
+        uint32_t diff = (off ^ offU) | (offEnd ^ endU);
+        asm volatile("" : "+v"(diff));
+        if (diff == 0u) {
+            /* the loop counter itself in an SGPR (offU..endU): no per-lane offset arithmetic (70 -> 68 VALU per
+             * pair, c2 -1.7 %). A wave-uniform loop like this one was mis-compiled inside the old nested draw loop;
+             * in the flat traversal loop it is correct (tools/stack_probe.py) */
+            for (uint32_t o = offU; o < endU; o += kBytes) {
+                PairHit ph;
+                if constexpr (PRIM) ph = rayTrianglePairP(ray, load_pairP_const(pbase, o));
+                else ph = rayTrianglePair(ray, load_pair_const(pbase, o));
+                count_tri<COUNT, DIAG>(cnt);
+                if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = o; }
+                count_tri<COUNT, DIAG>(cnt);
+                if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = o + 1u; }
+            }
+            off = offEnd;
+        }
+    }
+#endif
+    for (; off < offEnd; off += kBytes) {
+        const PairHit ph = test_at(off);
+#if WCPT_DUP_PAIR
+        if constexpr (!PRIM) {
+            Ray r2 = ray;
+            r2.origin.x = launder(r2.origin.x);
+            const PairHit p2 = rayTrianglePair(r2, load_pair_at(pbase, off));
+            sink(p2.t.x + p2.t.y);
+            sink_u((p2.hit0 ? 1u : 0u) | (p2.hit1 ? 2u : 0u));
+        }
+#endif
+        count_tri<COUNT, DIAG>(cnt);
+        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
+        count_tri<COUNT, DIAG>(cnt);
+        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+    }
+    if (tag != kNoTag) prim = 3u * (2u * (tag / kBytes) + (tag & 1u));
+    if (k < kfull) k = kfull;
+    if (k < kend) {
+        const PairHit ph = test_at((k >> 1) * kBytes);
+        count_tri<COUNT, DIAG>(cnt);
+        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
+    }
+}
+
 /* Leaf (:164-178): every triangle of the leaf at index positions [curLeft, curLeft + curCount), in index order,
  * taken iff accepted with t < rec.t (strict). UNIFORM: the leaf's whole pairs may be read with scalar loads (the
- * draw's record base must then be wave-uniform). */
+ * draw's record base must then be wave-uniform). primary: the segment is a sample's first (origin = the camera,
+ * wave-uniform), whose leaves are tested from the primary-ray pair records when the draw has them. */
 template <bool COUNT, bool DIAG, bool PAIRS, bool UNIFORM>
 __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uint32_t curLeft, uint32_t curCount,
-                                          float& rt, uint32_t& prim, Counters& cnt)
+                                          float& rt, uint32_t& prim, Counters& cnt, bool primary)
 {
     const uint32_t k0 = leaf_record(curLeft, curCount, g.ntri);
     if (PAIRS && k0 != kNoRecord) {
-        /* triangles [k0, kend) in pair records (2j, 2j+1): a leaf that starts in the second slot of a pair tests
-         * that pair for its first triangle, then whole pairs, then possibly the first slot of a last pair -- no
-         * per-iteration slot checks; applied in index order, strict < */
         const uint32_t kend = k0 + (curCount + 2u) / 3u;
-        uint32_t k = k0;
-        if (k & 1u) {
-            const PairHit ph = rayTrianglePair(ray, load_pair(g.tris, k >> 1));
-            count_tri<COUNT, DIAG>(cnt);
-            if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
-            k++;
-        }
-        /* whole pairs: one 32-bit byte-offset induction variable from the draw's record base, and the winner
-         * recorded as a tag -- the pair's offset for its first triangle, offset + 1 for its second -- decoded into
-         * the index position once per leaf */
-        const uint32_t kfull = kend & ~1u;
-        const WCPT_GLOBAL char* pbase = reinterpret_cast<const WCPT_GLOBAL char*>(g.tris);
-        const uint32_t offEnd = (kfull >> 1) * kPairRecordBytes;
-        uint32_t off = (k >> 1) * kPairRecordBytes, tag = kNoTag;
-#if WCPT_PAIR_UNIFORM
-        if (UNIFORM) {
-            /* Lanes whose whole-pair range equals the first active lane's (in a coherent wave: all of them) read
-             * the records at wave-uniform offsets with scalar loads: they go through the scalar cache (no per-lane
-             * addresses, no vector-memory return of 64 copies of the record) and the packed-FP32 instructions take
-             * the record straight from SGPRs (c2 -6 %). The other lanes take the per-lane loop below. */
-            const uint32_t offU = __builtin_amdgcn_readfirstlane(off);
-            const uint32_t endU = __builtin_amdgcn_readfirstlane(offEnd);
-            /* tested through an opaque value: a plain `off == offU` lets the compiler substitute the equal
-             * per-lane value back into the loads */
-            uint32_t diff = (off ^ offU) | (offEnd ^ endU);
-            asm volatile("" : "+v"(diff));
-            if (diff == 0u) {
-#if WCPT_PAIR_SLOOP
-                /* the loop counter itself in an SGPR (offU..endU): no per-lane offset arithmetic (70 -> 68 VALU per
-                 * pair, c2 -1.7 %). A wave-uniform loop like this one was mis-compiled inside the old nested draw
-                 * loop; in the flat traversal loop it is correct (tools/stack_probe.py) */
-                for (uint32_t o = offU; o < endU; o += kPairRecordBytes) {
-                    const PairHit ph = rayTrianglePair(ray, load_pair_const(pbase, o));
-                    count_tri<COUNT, DIAG>(cnt);
-                    if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = o; }
-                    count_tri<COUNT, DIAG>(cnt);
-                    if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = o + 1u; }
-                }
-                off = offEnd;
-#else
-                /* per-lane loop counter, offset re-derived with readfirstlane each iteration */
-                for (; off < offEnd; off += kPairRecordBytes) {
-                    const PairHit ph = rayTrianglePair(ray, load_pair_const(pbase, __builtin_amdgcn_readfirstlane(off)));
-                    count_tri<COUNT, DIAG>(cnt);
-                    if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
-                    count_tri<COUNT, DIAG>(cnt);
-                    if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
-                }
+#if WCPT_PRIMARY_PAIRS
+        if (primary && g.ptris != nullptr)
+            pair_leaf<COUNT, DIAG, UNIFORM, true>(ray, g.ptris, k0, kend, rt, prim, cnt);
+        else
 #endif
-            }
-        }
-#endif
-        for (; off < offEnd; off += kPairRecordBytes) {
-            const PairHit ph = rayTrianglePair(ray, load_pair_at(pbase, off));
-#if WCPT_DUP_PAIR
-            {
-                Ray r2 = ray;
-                r2.origin.x = launder(r2.origin.x);
-                const PairHit p2 = rayTrianglePair(r2, load_pair_at(pbase, off));
-                sink(p2.t.x + p2.t.y);
-                sink_u((p2.hit0 ? 1u : 0u) | (p2.hit1 ? 2u : 0u));
-            }
-#endif
-            count_tri<COUNT, DIAG>(cnt);
-            if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
-            count_tri<COUNT, DIAG>(cnt);
-            if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
-        }
-        if (tag != kNoTag) prim = 3u * (2u * (tag / kPairRecordBytes) + (tag & 1u));
-        if (k < kfull) k = kfull;
-        if (k < kend) {
-            const PairHit ph = rayTrianglePair(ray, load_pair(g.tris, k >> 1));
-            count_tri<COUNT, DIAG>(cnt);
-            if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
-        }
+            pair_leaf<COUNT, DIAG, UNIFORM, false>(ray, g.tris, k0, kend, rt, prim, cnt);
     } else {
         for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
             const uint32_t first = k + curLeft;
@@ -1042,7 +1129,7 @@ template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
                                          const wcpt_draw_command* __restrict__ draws,
                                          const uint64_t* __restrict__ tri_records, Stack& stk,
-                                         Counters& cnt, bool& overflow)
+                                         Counters& cnt, bool& overflow, bool primary)
 {
     float rt = kInfinity;
     uint32_t prim = kNoPrim, primDraw = 0;
@@ -1090,7 +1177,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)
                            ? (curCount > 0 ? kLeaf : kInterior) : kPop;
             if (mode == kLeaf) {
-                leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt);
+                leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt, primary);
                 mode = kPop;
             }
         }
@@ -1113,7 +1200,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         bool active = start_draw();
         while (active) {
             if (curCount > 0) {
-                leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt);
+                leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt, primary);
             } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)) {
                 continue;
             }
@@ -1281,8 +1368,11 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
     PathState ps;
     path_begin(ps, ray.origin, ray.direction);
     f3 L;
-    for (;;) {
-        const Hit h = intersect<COUNT, DIAG, PAIRS, SINGLE>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow);
+    /* segment counter of this sample: uniform across the wave's lanes (all start a sample together), so `primary`
+     * (segment 0: origin = the camera) is a wave-uniform branch condition */
+    for (uint32_t seg = 0;; seg++) {
+        const Hit h = intersect<COUNT, DIAG, PAIRS, SINGLE>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow,
+                                                           seg == 0u);
         const bool done = path_shade(ps, h, rng, sd, mats, L);
         phase_mark(cnt, 5);
         if (done) return L;

@@ -107,8 +107,17 @@ constexpr int kModeRender = 0, kModeCount = 1, kModeDiag = 2;
 /* Derived triangle records (pt_device.h): triangle k = index positions 3k..3k+2 stored as (a, b - a, c - a);
  * singles: 48 B per triangle; pairs: 80 B per triangle pair (2j, 2j+1). */
 constexpr uint32_t kSingleRecordBytes = 48, kPairRecordBytes = 80;
+/* primary-ray pair records (pt_device.h TriPairP), built with launch_build_primary_pairs; WCPT_PRIMARY_PAIRS=0 turns
+ * them off (the device then never finds a primary record address in the table) */
+constexpr uint32_t kPrimPairRecordBytes = 112;
+#ifndef WCPT_PRIMARY_PAIRS
+#define WCPT_PRIMARY_PAIRS 1
+#endif
 /* vertex_count bounds the vertex indices read (0xFFFFFFFF: unknown); a triangle with an index past it gets a NaN
  * record, which no ray accepts. */
+/* Primary-ray pair records (pt_device.h TriPairP) of `npairs` pair records for the camera origin (ox, oy, oz). */
+hipError_t launch_build_primary_pairs(const void* pairs, uint32_t npairs, float ox, float oy, float oz, void* out,
+                                      hipStream_t stream);
 hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles,
                                     uint32_t vertex_count, void* singles, void* pairs, hipStream_t stream);
 /* composite.comp (pt_composite.hip): gamma + PBR Neutral over `pixels` float4 texels into rgba32f or RGBA8 */

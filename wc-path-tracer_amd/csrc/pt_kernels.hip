@@ -180,6 +180,32 @@ __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restr
     o[4] = make_float4(v[0][8], v[1][8], 0.0f, 0.0f);
 }
 
+/* Primary-ray pair records from pair records (one thread per pair): the origin terms of both triangles with
+ * primary_terms, the same operations as rayTrianglePair's for that origin. */
+__global__ __launch_bounds__(256) void build_primary_pairs(const float4* __restrict__ pairs, uint32_t npairs, float ox,
+                                                           float oy, float oz, float4* __restrict__ out)
+{
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if (j >= npairs) return;
+    const float4* q = pairs + (uint64_t)kPairRecordFloat4s * j;
+    const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    /* pair record: (ax, ay) (az, e1x) (e1y, e1z) (e2x, e2y) (e2z, pad) as {tri 2j, tri 2j+1} float2 */
+    const float ax[2] = {r0.x, r0.y}, ay[2] = {r0.z, r0.w}, az[2] = {r1.x, r1.y}, e1x[2] = {r1.z, r1.w};
+    const float e1y[2] = {r2.x, r2.y}, e1z[2] = {r2.z, r2.w}, e2x[2] = {r3.x, r3.y}, e2y[2] = {r3.z, r3.w};
+    const float e2z[2] = {r4.x, r4.y};
+    float t[2][7];
+    for (int h = 0; h < 2; h++)
+        primary_terms(ox, oy, oz, ax[h], ay[h], az[h], e1x[h], e1y[h], e1z[h], e2x[h], e2y[h], e2z[h], t[h]);
+    float4* o = out + (uint64_t)kPrimPairFloat4s * j;
+    o[0] = make_float4(e1x[0], e1x[1], e1y[0], e1y[1]);
+    o[1] = make_float4(e1z[0], e1z[1], e2x[0], e2x[1]);
+    o[2] = make_float4(e2y[0], e2y[1], e2z[0], e2z[1]);
+    o[3] = make_float4(t[0][0], t[1][0], t[0][1], t[1][1]); /* oax, oay */
+    o[4] = make_float4(t[0][2], t[1][2], t[0][3], t[1][3]); /* oaz, qx */
+    o[5] = make_float4(t[0][4], t[1][4], t[0][5], t[1][5]); /* qy, qz */
+    o[6] = make_float4(t[0][6], t[1][6], 0.0f, 0.0f);       /* tq */
+}
+
 /* Device self-tests: evaluate the device definitions of the RNG and the deterministic libm on host inputs. */
 __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __restrict__ in, const uint32_t* __restrict__ in2,
                                                    uint32_t* __restrict__ out, uint32_t n)
@@ -295,6 +321,17 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
     const uint32_t npairs = (uint32_t)((triangles + 1ull) / 2ull);
     hipLaunchKernelGGL(dev::build_tri_records, dim3((npairs + 255u) / 256u), dim3(256), 0, stream, indices, vertices,
                        triangles, vertex_count, static_cast<float4*>(singles), static_cast<float4*>(pairs));
+    return hipGetLastError();
+}
+
+static_assert(dev::kPrimPairRecordBytes == kPrimPairRecordBytes, "primary-ray pair record size");
+static_assert(dev::kPairRecordBytes == kPairRecordBytes, "pair record size");
+hipError_t launch_build_primary_pairs(const void* pairs, uint32_t npairs, float ox, float oy, float oz, void* out,
+                                      hipStream_t stream)
+{
+    if (npairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::build_primary_pairs, dim3((npairs + 255u) / 256u), dim3(256), 0, stream,
+                       static_cast<const float4*>(pairs), npairs, ox, oy, oz, static_cast<float4*>(out));
     return hipGetLastError();
 }
 

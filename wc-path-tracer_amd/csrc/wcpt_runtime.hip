@@ -78,6 +78,14 @@ struct TriRecords {
     void* mem = nullptr;    /* single records, then pair records */
     uint64_t cap = 0;
     uint64_t pair_offset = 0;
+    uint64_t build_id = 0;  /* incremented on every rebuild of the records */
+    /* primary-ray pair records (pt_device.h TriPairP) for the camera position `porigin` (bit patterns), derived from
+     * the pair records of build `pbuild` */
+    void* pmem = nullptr;
+    uint64_t pcap = 0;
+    bool pvalid = false;
+    uint32_t porigin[3] = {0, 0, 0};
+    uint64_t pbuild = 0;
 };
 
 /* Pair records (packed two-triangle tests) pay off when leaves are fat: mean triangles per leaf >= this,
@@ -87,6 +95,8 @@ constexpr double kPairMinTrianglesPerLeaf = 4.0;
 /* Largest triangle count of a draw whose pair records are used: 40 B per triangle must stay addressable with 32-bit
  * byte offsets (2^26 triangles = 2.5 GiB of pair records); larger draws use single records. */
 constexpr uint64_t kPairMaxTriangles = 1ull << 26;
+/* Primary-ray pair records for the megakernel (pt_device.h WCPT_PRIMARY_PAIRS) */
+constexpr bool kPrimaryPairs = WCPT_PRIMARY_PAIRS != 0;
 
 hipError_t skewed_alloc(Buffer& b, uint64_t bytes)
 {
@@ -257,7 +267,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
     }
     if (ctx->tri.size() < n) ctx->tri.resize(n);
-    constexpr uint64_t W = 4; /* table words per draw (pt_device.h kTriTableWords) */
+    constexpr uint64_t W = 5; /* table words per draw (pt_device.h kTriTableWords) */
     bool table_dirty = ctx->tri_table.size() < W * n;
     if (table_dirty) ctx->tri_table.resize(W * n, 0);
     uint64_t tris_all = 0, leaves_all = 0, tris_max = 0;
@@ -305,6 +315,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
             t.gen_ib = gi;
             t.ntri = ntri;
             t.valid = true;
+            t.build_id++;
         }
         const uint64_t addr = reinterpret_cast<uint64_t>(t.mem);
         /* stack entries may carry the child's (left, count) when every node index and index position fits in 24
@@ -313,7 +324,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         const uint64_t nodes = bb ? (bb->bytes - o) / sizeof(wcpt_node) : ~0ull;
         uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
         if (dc[d].indexCount < (1u << 24)) flags |= 2u; /* pt_device.h kTriFlagIndex24 */
-        const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, flags};
+        const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, flags, ctx->tri_table[W * d + 4]};
         for (uint64_t w = 0; w < W; w++) {
             if (ctx->tri_table[W * d + w] != entry[w]) {
                 ctx->tri_table[W * d + w] = entry[w];
@@ -323,6 +334,48 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         tris_all += ntri;
         tris_max = std::max<uint64_t>(tris_max, ntri);
         leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
+    }
+    /* pair leaves address a draw's pair records with 32-bit byte offsets (pt_device.h load_pair_at) */
+    a.pair_records = tris_max <= kPairMaxTriangles &&
+                     (ctx->pair_records == 1 ||
+                      (ctx->pair_records < 0 && leaves_all > 0 && (double)tris_all >= kPairMinTrianglesPerLeaf * leaves_all));
+    /* primary-ray pair records (megakernel with pair records): derived once per camera position and records build */
+    const bool want_primary = kPrimaryPairs && a.pair_records && ctx->kernel == WCPT_KERNEL_MEGAKERNEL;
+    uint32_t origin[3];
+    std::memcpy(origin, sd.position, sizeof(origin));
+    for (uint32_t d = 0; d < n; d++) {
+        TriRecords& t = ctx->tri[d];
+        uint64_t paddr = 0;
+        if (want_primary && t.ntri > 0) {
+            const uint64_t npairs = (uint64_t)t.ntri / 2u + 1u;
+            const uint64_t bytes = npairs * wcpt::kPrimPairRecordBytes;
+            const bool fresh = t.pvalid && t.pbuild == t.build_id && std::memcmp(t.porigin, origin, sizeof(origin)) == 0;
+            if (!fresh) {
+                if (t.pcap < bytes) {
+                    if (t.pmem) {
+                        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+                        (void)hipFree(t.pmem);
+                    }
+                    t.pmem = nullptr;
+                    t.pcap = 0;
+                    t.pvalid = false;
+                    HIP_TRY(ctx, hipMalloc(&t.pmem, bytes), "hipMalloc(primary-ray pair records)");
+                    t.pcap = bytes;
+                }
+                HIP_TRY(ctx, wcpt::launch_build_primary_pairs(static_cast<const char*>(t.mem) + t.pair_offset,
+                                                              (uint32_t)npairs, sd.position[0], sd.position[1],
+                                                              sd.position[2], t.pmem, ctx->stream),
+                        "build_primary_pairs");
+                t.pvalid = true;
+                t.pbuild = t.build_id;
+                std::memcpy(t.porigin, origin, sizeof(origin));
+            }
+            paddr = reinterpret_cast<uint64_t>(t.pmem);
+        }
+        if (ctx->tri_table[W * d + 4] != paddr) {
+            ctx->tri_table[W * d + 4] = paddr;
+            table_dirty = true;
+        }
     }
     if (ctx->tri_table_cap < n) {
         if (ctx->d_tri_table) {
@@ -341,10 +394,6 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(triangle record table)");
     }
     a.tri_records = ctx->d_tri_table;
-    /* pair leaves address a draw's pair records with 32-bit byte offsets (pt_device.h load_pair_at) */
-    a.pair_records = tris_max <= kPairMaxTriangles &&
-                     (ctx->pair_records == 1 ||
-                      (ctx->pair_records < 0 && leaves_all > 0 && (double)tris_all >= kPairMinTrianglesPerLeaf * leaves_all));
     return WCPT_SUCCESS;
 }
 
@@ -506,8 +555,10 @@ int wcpt_destroy(wcpt_context* ctx)
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     wcpt::wf_release(ctx->wf);
-    for (auto& t : ctx->tri)
+    for (auto& t : ctx->tri) {
         if (t.mem) (void)hipFree(t.mem);
+        if (t.pmem) (void)hipFree(t.pmem);
+    }
     if (ctx->d_tri_table) (void)hipFree(ctx->d_tri_table);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     for (auto& p : ctx->events) {
