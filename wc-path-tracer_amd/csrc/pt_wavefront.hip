@@ -157,6 +157,9 @@ constexpr int wf_lds_per_wave(int n) { return n * 512; }
 constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
 
+#ifndef WCPT_WF_TRACE_SHARE
+#define WCPT_WF_TRACE_SHARE 1
+#endif
 #ifndef WCPT_WF_REC_OFF24
 #define WCPT_WF_REC_OFF24 1
 #endif
@@ -767,7 +770,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
         if (e != hipSuccess) return e;
         if (bpc < 1) bpc = 1;
     }
-    const uint32_t trace_grid = (uint32_t)(bpc * cus);
+    uint32_t trace_grid = (uint32_t)(bpc * cus);
 /* Shade blocks per CU (grid-stride over the queue). The continuing paths are appended in roughly the order
  * the blocks walk their chunks, so a small grid keeps the next queue close to the input order (coherent rays
  * for the next trace). Measured on c3: 4 -> 7.98 ms, 8 -> 8.13, 16 -> 8.56, 32 -> 8.98, one thread per slot ->
@@ -784,6 +787,12 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     if (sort_rays || mode == kModeDiag) K = 1; /* one sort scratch and one diagnostics block */
     const uint32_t tiles = tilesX * tilesY;
     if (K > tiles) K = tiles;
+#if WCPT_WF_TRACE_SHARE
+    /* each pipeline's persistent trace grid holds 1/K of the resident-wave slots, so the K traces run side by side
+     * instead of the first one taking every slot and the others only filling its tail (c3 6.58 -> 6.16 ms with two
+     * pipelines; 5/8 or 3/4 of the slots per pipeline measured equal, 7/16 slower) */
+    if (K > 1) trace_grid = trace_grid / K > 0 ? trace_grid / K : 1u;
+#endif
     e = wf_reserve_result(w, (uint64_t)a.W * a.rows);
     if (e != hipSuccess) return e;
     if (K == 1) return launch_pipe(a, mode, s0, s0, w.result, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream);
