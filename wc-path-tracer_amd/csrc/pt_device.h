@@ -502,9 +502,6 @@ constexpr uint32_t kNoTag = 0xFFFFFFFFu;
 #ifndef WCPT_PAIR_SLOOP
 #define WCPT_PAIR_SLOOP 1
 #endif
-#ifndef WCPT_PAIR_UNIFORM_ENDS
-#define WCPT_PAIR_UNIFORM_ENDS 0
-#endif
 
 __device__ __forceinline__ TriPair load_pair_at(const WCPT_GLOBAL char* base, uint32_t off)
 {
@@ -932,39 +929,6 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         if constexpr (PRIM) return rayTrianglePairP(ray, load_pairP_at(pbase, off));
         else return rayTrianglePair(ray, load_pair_at(pbase, off));
     };
-#if WCPT_PAIR_UNIFORM && WCPT_PAIR_UNIFORM_ENDS
-    if (UNIFORM) {
-        /* The whole leaf in the scalar loop: pairs k0 >> 1 .. (kend - 1) >> 1, including a first pair whose slot 0
-         * (triangle k0 - 1) and a last pair whose slot 1 (triangle kend) belong to another leaf or lie past the
-         * records; those slots are masked by wave-uniform (SGPR) offset tests, so the peeled first / last pair tests
-         * with per-lane loads disappear for lanes that share the first active lane's leaf. Same tests, same order. */
-        const uint32_t lo = (k0 >> 1) * kBytes, hi = ((kend + 1u) >> 1) * kBytes;
-        const uint32_t loU = __builtin_amdgcn_readfirstlane(lo), hiU = __builtin_amdgcn_readfirstlane(hi);
-        const uint32_t k0U = __builtin_amdgcn_readfirstlane(k0), kendU = __builtin_amdgcn_readfirstlane(kend);
-        uint32_t diff = (k0 ^ k0U) | (kend ^ kendU);
-        asm volatile("" : "+v"(diff));
-        if (diff == 0u) {
-            const uint32_t skip0 = (k0U & 1u) ? loU : 0xFFFFFFFFu;           /* slot 0 of the first pair */
-            const uint32_t skip1 = (kendU & 1u) ? hiU - kBytes : 0xFFFFFFFFu; /* slot 1 of the last pair */
-            uint32_t tag = kNoTag;
-            for (uint32_t o = loU; o < hiU; o += kBytes) {
-                PairHit ph;
-                if constexpr (PRIM) ph = rayTrianglePairP(ray, load_pairP_const(pbase, o));
-                else ph = rayTrianglePair(ray, load_pair_const(pbase, o));
-                if (o != skip0) {
-                    count_tri<COUNT, DIAG>(cnt);
-                    if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = o; }
-                }
-                if (o != skip1) {
-                    count_tri<COUNT, DIAG>(cnt);
-                    if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = o + 1u; }
-                }
-            }
-            if (tag != kNoTag) prim = 3u * (2u * (tag / kBytes) + (tag & 1u));
-            return;
-        }
-    }
-#endif
     uint32_t k = k0;
     if (k & 1u) {
         const PairHit ph = test_at((k >> 1) * kBytes);
