@@ -1275,10 +1275,20 @@ __device__ __forceinline__ void path_begin(PathState& ps, f3 origin, f3 dir)
 #ifndef WCPT_SHADE_SHARED
 #define WCPT_SHADE_SHARED 1
 #endif
+/* The last segment of a pixel's last sample ends the path whatever it samples next: after its emission term
+ * (:253) the reference still draws the BSDF sample of :256-280 -- the next direction, transmittance and RNG state --
+ * but the loop then exits (:245, :283) and nothing reads them again (the RNG state carries over only into a next
+ * sample, :309-310). WCPT_LAST_SEGMENT_SHORTCUT=1 returns right after the emission term there: the same radiance
+ * bits, without the dead RandomDirection, reflection, normalize and 1/direction. The condition is wave-uniform in
+ * the megakernel (the lanes of a wave start every sample together). */
+#ifndef WCPT_LAST_SEGMENT_SHORTCUT
+#define WCPT_LAST_SEGMENT_SHORTCUT 1
+#endif
 /* Shading after an Intersect (pathTracer.comp:248-280). Returns true when the path is finished, with its
- * radiance in L: on a miss (:248-249) or when the bounce loop is exhausted (:245, :283). */
+ * radiance in L: on a miss (:248-249) or when the bounce loop is exhausted (:245, :283). lastSample: this is the
+ * pixel's last sample (its RNG state is not read after the path). */
 __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t& rng, const wcpt_scene_data& sd,
-                                           const wcpt_material* __restrict__ mats, f3& L)
+                                           const wcpt_material* __restrict__ mats, f3& L, bool lastSample)
 {
     Ray& ray = ps.ray;
     if (!h.hit) {
@@ -1291,6 +1301,14 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
     const float emissionStrength = m.emissionStrength;
     const float roughness = m.roughness;
     ps.totalLight = ps.totalLight + (emission * emissionStrength) * ps.transmittance;
+#if WCPT_LAST_SEGMENT_SHORTCUT
+    if (lastSample && ps.bounce + 1u > sd.maxBounceCount) { /* the loop's last iteration (:245): nothing below is read */
+        L = ps.totalLight;
+        return true;
+    }
+#else
+    (void)lastSample;
+#endif
 
 #if WCPT_SHADE_SHARED
     /* Both branches of :256-280 end in normalize(base + roughness * RandomDirection(rng)) and a new 1/direction.
@@ -1374,7 +1392,7 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
                                        const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
                                        const wcpt_draw_command* __restrict__ draws,
                                        const uint64_t* __restrict__ tri_records, Stack& stk,
-                                       Counters& cnt, bool& overflow)
+                                       Counters& cnt, bool& overflow, bool lastSample)
 {
     PathState ps;
     path_begin(ps, ray.origin, ray.direction);
@@ -1384,7 +1402,7 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
     for (uint32_t seg = 0;; seg++) {
         const Hit h = intersect<COUNT, DIAG, PAIRS, SINGLE>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow,
                                                            seg == 0u);
-        const bool done = path_shade(ps, h, rng, sd, mats, L);
+        const bool done = path_shade(ps, h, rng, sd, mats, L, lastSample);
         phase_mark(cnt, 5);
         if (done) return L;
     }

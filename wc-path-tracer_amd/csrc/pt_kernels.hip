@@ -66,7 +66,8 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
         r.origin = origin;
         r.direction = dir;
         r.invDirection = rcp3(dir);
-        result = result + TraceRay<COUNT, DIAG, PAIRS, SINGLE>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow);
+        result = result + TraceRay<COUNT, DIAG, PAIRS, SINGLE>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow,
+                                                       s + 1u == sd.samples);
     }
     result = result / (float)sd.samples; /* :312 */
     if (!COUNT) {

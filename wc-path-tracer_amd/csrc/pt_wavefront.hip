@@ -440,7 +440,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
             const Hit h = resolve_hit(ps.ray, hi.x, prim, __float_as_uint(hi.z), spheres, draws, tri_records);
             if (COUNT && h.hit) cnt.hits++;
             f3 L;
-            if (!path_shade(ps, h, seed, sd, mats, L)) {
+            if (!path_shade(ps, h, seed, sd, mats, L, sample + 1u == sd.samples)) {
                 cont = true;
             } else {
                 const float4 rs = b.result[p];
