@@ -98,6 +98,10 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
     return slot;
 }
 
+#ifndef WCPT_WF_ANYHIT_LAST
+#define WCPT_WF_ANYHIT_LAST 1
+#endif
+
 /* ---- ray generation ------------------------------------------------------------------------------- */
 template <bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
@@ -249,6 +253,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     uint32_t p = 0, d = 0, prim = kNoPrim, primDraw = 0;
     uint32_t ca = 0, cb = 0, cr = 0, mode = kModeDone;
     float rt = kInfinity;
+    bool any = false; /* this ray is the last segment of its pixel's last sample (render build only) */
     Ray ray;
     uint64_t tim[kDiagTimers] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tprev = DIAG ? __builtin_amdgcn_s_memtime() : 0;
@@ -297,7 +302,17 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 if (take) {
                     p = b.order ? b.order[lo + rank] : lo + rank;   /* input slot: consecutive lanes, consecutive slots */
                     const float4 r0 = b.in.ray0[p];
+#if WCPT_WF_ANYHIT_LAST
+                    const float4 r1 = b.in.ray1[p];
+                    /* path_shade's last-segment shortcut keeps only the material of this segment's hit, and every
+                     * triangle carries material 0 (:175): whether some triangle is accepted below the sphere loop's
+                     * rec.t is all that is read. Up to the first acceptance the traversal is the reference's, so the
+                     * ray finishes there; its lane takes the next queued ray. */
+                    any = !COUNT && WCPT_LAST_SEGMENT_SHORTCUT && __float_as_uint(r1.z) + 1u > sd.maxBounceCount &&
+                          __float_as_uint(r1.w) + 1u == sd.samples;
+#else
                     const float2 r1 = reinterpret_cast<const float2*>(b.in.ray1)[2u * p];
+#endif
                     const float4 pr = b.in.pre[p];
                     ray.origin = mk3(r0.x, r0.y, r0.z);
                     ray.direction = mk3(r0.w, r1.x, r1.y);
@@ -380,7 +395,8 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     cnt.triangle_tests++;
                     simd_step<DIAG>(cnt.wave_tri, cnt.lane_tri);
                 }
-                if (tt != -1.0f && tt < rt) {
+                const bool acc = tt != -1.0f && tt < rt;
+                if (acc) {
                     rt = tt;
                     prim = ca;
                     primDraw = d;
@@ -388,6 +404,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 ca += 3;
                 cr += (cr != kNoRecord) ? 48u : 0u;
                 if (ca >= cb) mode = kModePop;
+                if (acc && any) mode = kModeDone; /* any-hit segment: its answer is fixed */
             }
             diag_mark<DIAG>(tim, tprev, 1);
             if (has && mode == kModeDone) {
