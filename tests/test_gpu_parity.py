@@ -646,6 +646,26 @@ def test_edge_inputs_match_oracle(gpu_ctx, kernel, kind, bounces, spp):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("bounces,spp", [(0, 1), (2, 2), (4, 1), (3, 3)])
+def test_last_segment_shortcuts_match_oracle(gpu_ctx, kernel, bounces, spp):
+    """The last segment of a pixel's last sample ends after its emission term (WCPT_LAST_SEGMENT_SHORTCUT) and the
+    wavefront traces it as any-hit (WCPT_WF_ANYHIT_LAST): exact only because every triangle carries material 0
+    (:175). Material 0 is made emissive here, so the triangle answer of that segment reaches the image, and
+    samples > 1 checks that only the last sample takes the shortcut (its RNG state feeds the next sample)."""
+    import copy
+    s = copy.copy(get_scene("cornell"))
+    m = s.materials.copy()
+    m["emission"][0] = (0.3, 0.2, 0.1)
+    m["emissionStrength"][0] = 1.5
+    s.materials = m
+    W, H = 48, 40
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, kernel=kernel)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("refs", [1, 0])
 def test_stack_refs_match_oracle(gpu_ctx, kernel, refs):
     """Stack entries carrying (left, count) (default) or node indices: same frame, same counters. The hand-made
