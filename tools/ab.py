@@ -66,7 +66,7 @@ def main():
             ctx.set_option(wcpt._lib.OPTION_WF_STACK, int(o.get("lds", 10)))
             ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, int(o.get("pairs", -1)))
             ctx.set_option(wcpt._lib.OPTION_PACKED_REFS, int(o.get("refs", 1)))
-            ctx.set_option(wcpt._lib.OPTION_WF_REFILL, int(o.get("refill", 20)))
+            ctx.set_option(wcpt._lib.OPTION_WF_REFILL, int(o.get("refill", wcpt._lib.DEFAULT_WF_REFILL)))
             ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, int(o.get("order", 2)))
             ctx.set_option(wcpt._lib.OPTION_WF_PIPES, int(o.get("pipes", wcpt._lib.DEFAULT_WF_PIPES)))
             dev = scenes[o.get("deindex", "0")]

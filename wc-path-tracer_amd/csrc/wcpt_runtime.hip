@@ -140,7 +140,7 @@ struct wcpt_context {
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
-    int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (c3: 12 -> 6.83 ms, 20..32 -> 6.73, 48 -> 7.03) */
+    int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (round 2 with the any-hit last segment, c3: 4 / 8 / 12 / 16 / 20 -> 5.80 / 5.74 / 5.71 / 5.75 / 5.80 ms) */
 #ifndef WCPT_WF_PIPES_DEFAULT
 #define WCPT_WF_PIPES_DEFAULT 2
 #endif
