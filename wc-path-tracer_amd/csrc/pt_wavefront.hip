@@ -98,6 +98,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
     return slot;
 }
 
+#ifndef WCPT_WF_PUSH_CULL
+#define WCPT_WF_PUSH_CULL 1
+#endif
 #ifndef WCPT_WF_ANYHIT_LAST
 #define WCPT_WF_ANYHIT_LAST 1
 #endif
@@ -373,9 +376,13 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 const bool leftFirst = leftDist < rightDist;
                 const bool passNear = leftFirst ? passL : passR;
                 const bool passFar = leftFirst ? passR : passL;
-                if (passFar) {
+                /* A far child whose entry distance already exceeds rec.t would be culled at its pop (:162): rec.t
+                 * only shrinks, so the render build does not push it (the counting build keeps the reference's
+                 * pushes and pops). */
+                const float farT0 = leftFirst ? r0 : l0;
+                if (passFar && (COUNT || !WCPT_WF_PUSH_CULL || !(farT0 > rt))) {
                     const NodeV& F = leftFirst ? R : L;
-                    if (!stk.push(node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w), leftFirst ? r0 : l0))
+                    if (!stk.push(node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w), farT0))
                         overflow = true;
                 }
                 if (passNear && !((leftFirst ? l0 : r0) > rt)) {
