@@ -919,9 +919,19 @@ __device__ __forceinline__ DrawGeom draw_geom(const wcpt_draw_command* __restric
  * for its first triangle, then whole pairs, then possibly the first slot of a last pair -- no per-iteration slot
  * checks; applied in index order, strict <. UNIFORM: lanes of a coherent wave walk the whole pairs with scalar loads
  * (the record base must be wave-uniform). */
+/* The pair record last tested for a peeled (odd-boundary) triangle in this segment: a leaf that ends in slot 0 of a pair
+ * and the leaf that starts in its slot 1 (two 17-triangle midpoint leaves share the pair (16, 17)) both need that
+ * record's test. Its byte offset with the two acceptance bits in bits 0-1, and both t: the second leaf reuses the
+ * values the first computed -- the same test of the same ray on the same record -- and still applies them against
+ * its own rec.t in its own order. Reset per segment and per draw (the offsets are relative to a draw's records). */
+#ifndef WCPT_PEEL_CACHE
+#define WCPT_PEEL_CACHE 1
+#endif
+struct PeelCache { uint32_t tag; v2f t; };
+constexpr uint32_t kNoPeel = 0xFFFFFFFFu;
 template <bool COUNT, bool DIAG, bool UNIFORM, bool PRIM>
 __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_t k0, uint32_t kend, float& rt,
-                                          uint32_t& prim, Counters& cnt)
+                                          uint32_t& prim, Counters& cnt, PeelCache& pc)
 {
     constexpr uint32_t kBytes = PRIM ? kPrimPairRecordBytes : kPairRecordBytes;
     const WCPT_GLOBAL char* pbase = reinterpret_cast<const WCPT_GLOBAL char*>(recs);
@@ -929,9 +939,28 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         if constexpr (PRIM) return rayTrianglePairP(ray, load_pairP_at(pbase, off));
         else return rayTrianglePair(ray, load_pair_at(pbase, off));
     };
+    /* the peeled pair at `off`, through the per-segment cache */
+    auto peeled_at = [&](uint32_t off) {
+#if WCPT_PEEL_CACHE
+        PairHit ph;
+        if ((pc.tag & ~3u) == off) {
+            ph.t = pc.t;
+            ph.hit0 = (pc.tag & 1u) != 0u;
+            ph.hit1 = (pc.tag & 2u) != 0u;
+        } else {
+            ph = test_at(off);
+            pc.tag = off | (ph.hit0 ? 1u : 0u) | (ph.hit1 ? 2u : 0u);
+            pc.t = ph.t;
+        }
+        return ph;
+#else
+        (void)pc;
+        return test_at(off);
+#endif
+    };
     uint32_t k = k0;
     if (k & 1u) {
-        const PairHit ph = test_at((k >> 1) * kBytes);
+        const PairHit ph = peeled_at((k >> 1) * kBytes);
         count_tri<COUNT, DIAG>(cnt);
         if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
         k++;
@@ -1001,7 +1030,7 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
     if (tag != kNoTag) prim = 3u * (2u * (tag / kBytes) + (tag & 1u));
     if (k < kfull) k = kfull;
     if (k < kend) {
-        const PairHit ph = test_at((k >> 1) * kBytes);
+        const PairHit ph = peeled_at((k >> 1) * kBytes);
         count_tri<COUNT, DIAG>(cnt);
         if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
     }
@@ -1013,17 +1042,17 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
  * wave-uniform), whose leaves are tested from the primary-ray pair records when the draw has them. */
 template <bool COUNT, bool DIAG, bool PAIRS, bool UNIFORM>
 __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uint32_t curLeft, uint32_t curCount,
-                                          float& rt, uint32_t& prim, Counters& cnt, bool primary)
+                                          float& rt, uint32_t& prim, Counters& cnt, bool primary, PeelCache& pc)
 {
     const uint32_t k0 = leaf_record(curLeft, curCount, g.ntri);
     if (PAIRS && k0 != kNoRecord) {
         const uint32_t kend = k0 + (curCount + 2u) / 3u;
 #if WCPT_PRIMARY_PAIRS
         if (primary && g.ptris != nullptr)
-            pair_leaf<COUNT, DIAG, UNIFORM, true>(ray, g.ptris, k0, kend, rt, prim, cnt);
+            pair_leaf<COUNT, DIAG, UNIFORM, true>(ray, g.ptris, k0, kend, rt, prim, cnt, pc);
         else
 #endif
-            pair_leaf<COUNT, DIAG, UNIFORM, false>(ray, g.tris, k0, kend, rt, prim, cnt);
+            pair_leaf<COUNT, DIAG, UNIFORM, false>(ray, g.tris, k0, kend, rt, prim, cnt, pc);
     } else {
         for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
             const uint32_t first = k + curLeft;
@@ -1170,6 +1199,9 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     phase_mark(cnt, 1);
 
     uint32_t curLeft = 0, curCount = 0;
+    PeelCache pc;
+    pc.tag = kNoPeel;
+    pc.t = bc2(0.0f);
     if constexpr (SINGLE) {
         const DrawGeom g = draw_geom<PAIRS>(draws, tri_records, 0);
         /* one traversal step per iteration as sequential ifs on the lane's mode (pop -> interior -> leaf), like
@@ -1188,7 +1220,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)
                            ? (curCount > 0 ? kLeaf : kInterior) : kPop;
             if (mode == kLeaf) {
-                leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt, primary);
+                leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
                 mode = kPop;
             }
         }
@@ -1203,6 +1235,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
                 rt_before = rt;
                 if (root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
                     stk.reset();
+                    pc.tag = kNoPeel; /* offsets of another draw's records */
                     return true;
                 }
             }
@@ -1211,7 +1244,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         bool active = start_draw();
         while (active) {
             if (curCount > 0) {
-                leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt, primary);
+                leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
             } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)) {
                 continue;
             }
