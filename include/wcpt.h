@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define WCPT_ABI_VERSION 1
+/* 2: wcpt_counters gained ref_stack_overflow_segments / ref_stack_max; the wcpt_group_* multi-device entry points */
+#define WCPT_ABI_VERSION 2
 
 /* ---- error codes (VkResult-compatible where a VkResult exists) ---------------------------------- */
 #define WCPT_SUCCESS                      0
@@ -182,6 +183,14 @@ typedef struct wcpt_counters {
     uint64_t wave_interior_steps, lane_interior_steps;
     uint64_t wave_triangle_steps, lane_triangle_steps;
     uint64_t wave_segment_steps, lane_segment_steps;
+    /* The reference's traversal stack is `uint nodeStack[32]` (pathTracer.comp:151), pushed with the root (:155) and
+     * both children of every interior node that survives its box test (:192-198). Counted exactly for the same frame
+     * (ABI version 2): segments in which the reference writes nodeStack[32] or beyond -- undefined behaviour in the
+     * reference, whose result for those rays has no reference meaning -- and the deepest stack the reference reaches
+     * (entries after a push; UINT64_MAX if the tree was too deep to track, > 64 levels). This implementation's own
+     * stack (48 entries, far children only) is unaffected by either. */
+    uint64_t ref_stack_overflow_segments;
+    uint64_t ref_stack_max;
 } wcpt_counters;
 
 /* Host mesh produced by the OBJ loader (ModelLoader.jai:60-141) or a scene generator. Memory is owned
@@ -239,11 +248,18 @@ uint64_t wcpt_image_device_ptr(wcpt_context* ctx);                 /* float4[row
  * context-owned image. The caller keeps ownership. */
 int      wcpt_set_external_image(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes);
 /* Gather payload written by the render itself: every wcpt_render also stores each pixel it
- * finishes into caller-owned device memory at `device_ptr` -- row-major float[rows][width][channels], channels 3
- * (RGB; alpha is always 1.0, pathTracer.comp:323) or 4 (RGBA) -- the same values as the accumulation image. A
- * multi-GPU host points it at the buffer it hands to the collective, so no copy kernel sits between the render and
- * the gather. `bytes` must hold width*rows*channels*4 at render time. device_ptr == 0 turns it off. Takes effect
- * for the next render; no synchronisation. The caller keeps ownership. */
+ * finishes into caller-owned device memory at `device_ptr`, row-major [rows][width], in payload format `channels`:
+ *   WCPT_PAYLOAD_RGB32F (3)  float RGB, the accumulation image's values (alpha is always 1.0, pathTracer.comp:323);
+ *   WCPT_PAYLOAD_RGBA32F (4) float RGBA, the accumulation image's values (16-byte aligned);
+ *   WCPT_PAYLOAD_DISPLAY_RGBA8 (8) the display step of composite.comp:36-53 (gamma 1/2.2 + PBR Neutral, UNORM8 as
+ *     wcpt_composite's RGBA8) of the accumulated value, 4 B/px: a presented multi-device frame at a quarter of the
+ *     float payload's bytes, with no separate composite pass.
+ * A multi-GPU host points it at the buffer it hands to the collective, so no copy kernel sits between the render and
+ * the gather. `bytes` must hold width*rows*(bytes per pixel) at render time. device_ptr == 0 turns it off. Takes
+ * effect for the next render; no synchronisation. The caller keeps ownership. */
+#define WCPT_PAYLOAD_RGB32F        3
+#define WCPT_PAYLOAD_RGBA32F       4
+#define WCPT_PAYLOAD_DISPLAY_RGBA8 8
 int      wcpt_set_gather_output(wcpt_context* ctx, uint64_t device_ptr, uint64_t bytes, uint32_t channels);
 int      wcpt_readback(wcpt_context* ctx, float* dst, uint64_t bytes);
 int      wcpt_image_upload(wcpt_context* ctx, const float* src, uint64_t bytes); /* seed accumulation */
@@ -271,6 +287,39 @@ int      wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, u
 /* Wavefront trace-loop phase timers of the last wcpt_render_counters call with WCPT_OPTION_DIAGNOSTICS set
  * (s_memtime cycles summed over waves): {fetch, leaf, interior, pop, epilogue, waves, iterations, -}. */
 int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
+
+/* ---- one frame on several devices from one host thread ------------------------------- */
+/* The reference host is one process and one thread (main.jai:185-194) driving Render (PathTracingRenderer.jai:399).
+ * A group keeps that shape for N devices: one context per device, rank r rendering rows [r*H/N, (r+1)*H/N) of the
+ * frame with unchanged global pixel indices and seeds (so the frame equals a one-device render bit for bit), and an
+ * RCCL communicator over the devices (ncclCommInitAll, rccl.h:236) for the one exchange: each frame's row blocks
+ * go to the root device over xGMI as grouped ncclSend/ncclRecv (rccl.h:700,722; blocks may differ by a row).
+ *   wcpt_group_create      devices[0..n) distinct device ordinals; `root` is the rank that receives the frame.
+ *   wcpt_group_context     rank r's context: upload that device's copy of the scene with wcpt_buffer_* and set
+ *                          kernels/options on it, as for a single context. Owned by the group.
+ *   wcpt_group_create_screen  CreateScreen/Resize for the whole frame (each rank allocates only its row block).
+ *   wcpt_group_set_output  where the presented frame goes: device memory on the root device (e.g.
+ *                          wcpt_buffer_device_address of a root-context buffer) of width*height*(payload bytes per
+ *                          pixel), row-major, in WCPT_PAYLOAD_* format; dst == 0 turns presenting off (the ranks
+ *                          keep accumulating their blocks). The root renders its own block straight into it; the
+ *                          other ranks' renders write their blocks into group-owned payload buffers (no copy pass).
+ *   wcpt_group_render      Render on every rank (scene by value; materials/spheres/draw_commands are arrays of n
+ *                          device addresses, rank r's in [r]), then, with an output set, the gather of this frame on
+ *                          the ranks' streams. Asynchronous, like wcpt_render.
+ *   wcpt_group_sync        waits for every rank (and reports a traversal-stack overflow on any of them).
+ * Errors leave the group usable; wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains them. */
+typedef struct wcpt_group wcpt_group;
+int           wcpt_group_create(const int* devices, int n, int root, wcpt_group** out);
+int           wcpt_group_destroy(wcpt_group* g);
+wcpt_context* wcpt_group_context(wcpt_group* g, int rank);
+int           wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height);
+int           wcpt_group_set_output(wcpt_group* g, int format, uint64_t dst, uint64_t bytes);
+int           wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_t* materials,
+                                const uint64_t* spheres, const uint64_t* draw_commands);
+int           wcpt_group_sync(wcpt_group* g);
+
+/* HIP runtime version the library runs on (hipRuntimeGetVersion), e.g. 70226090 for ROCm 7.2. */
+int      wcpt_runtime_version(int* version);
 
 /* ---- kernel timing (HIP events on the context's stream) -------------------------------------------- */
 int      wcpt_profile_begin(wcpt_context* ctx);
@@ -309,7 +358,8 @@ void     wcpt_string_free(char* text);
  * every input, 12 = as 8 for the kernels' reciprocals (rcp_exact, and its packed pair form on (x, ~x)),
  * 13 = how many inputs of the block fail the fast result's class check (take the general division),
  * 14 = the two triangle acceptance forms on (u, v) = (in, in2) with t = 1 (bit 0 compares, bit 1 minimum3),
- * 15 = as 8 for the kernels' square root (sqrt_exact) against the correctly rounded sqrtf. Host arrays of 32-bit words. */
+ * 15 = as 8 for the kernels' square root (sqrt_exact) against the correctly rounded sqrtf,
+ * 16 = the kernels' GLSL vector / scalar on one component: in * RN(1 / in2). Host arrays of 32-bit words. */
 int      wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const uint32_t* in2,
                               uint32_t* out, uint32_t n);
 

@@ -15,13 +15,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 SCENE_DATA_ITEMSIZE = 164
-COUNTER_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",
-                  "hits", "draw_fetches")
+WORK_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",
+               "hits", "draw_fetches")
+REF_STACK_FIELDS = ("ref_stack_overflow_segments", "ref_stack_max")
+COUNTER_FIELDS = WORK_FIELDS + REF_STACK_FIELDS
 
 
 class _Counters(C.Structure):
-    # wcpt_counters of include/wcpt.h: the 8 reference counters + 6 implementation diagnostics (left 0 here)
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS] + [(f"_diag{i}", C.c_uint64) for i in range(6)]
+    # wcpt_counters of include/wcpt.h: the 8 reference counters + 6 implementation diagnostics (left 0 here) + the
+    # reference-stack fields (segments writing past uint nodeStack[32], deepest stack)
+    _fields_ = ([(n, C.c_uint64) for n in WORK_FIELDS] + [(f"_diag{i}", C.c_uint64) for i in range(6)]
+                + [(n, C.c_uint64) for n in REF_STACK_FIELDS])
 
 
 class _Draw(C.Structure):

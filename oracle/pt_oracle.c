@@ -226,11 +226,16 @@ static HitInfo Intersect(Scene* S, const Ray* ray)
         }
     }
 
+    /* The reference's stack is uint nodeStack[32] (:151). This one is deeper, so the reference's out-of-bounds writes
+     * are counted instead of performed: a segment that pushes at index >= 32 (ref_stack_overflow_segments), and the
+     * deepest stack reached (ref_stack_max). */
+    int ref_overflow = 0;
     for (uint32_t i = 0; i < sd->drawCommandCount; i++) {
         const oracle_draw* dc = &S->draws[i];
         int stackIndex = 0;
         S->cnt->draw_fetches++;
         nodeStack[stackIndex++] = 0;
+        if (S->cnt->ref_stack_max < 1) S->cnt->ref_stack_max = 1;
         while (stackIndex > 0) {
             const uint32_t nodeIdx = nodeStack[--stackIndex];
             const wcpt_node* node = &dc->bvh[nodeIdx];
@@ -262,6 +267,8 @@ static HitInfo Intersect(Scene* S, const Ray* ray)
                 const float leftDist = (leftT.x > 0.0f) ? leftT.x : leftT.y;
                 const float rightDist = (rightT.x > 0.0f) ? rightT.x : rightT.y;
                 S->cnt->interior_visits++;
+                if (stackIndex + 2 > 32) ref_overflow = 1;
+                if ((uint64_t)(stackIndex + 2) > S->cnt->ref_stack_max) S->cnt->ref_stack_max = (uint64_t)(stackIndex + 2);
                 if (stackIndex + 2 > ORACLE_STACK) { S->overflow = 1; continue; }
                 if (leftDist < rightDist) {
                     nodeStack[stackIndex++] = rightChild;
@@ -274,6 +281,7 @@ static HitInfo Intersect(Scene* S, const Ray* ray)
         }
     }
 
+    S->cnt->ref_stack_overflow_segments += (uint64_t)ref_overflow;
     if (rec.hit) {
         rec.p = add3(ray->origin, smul3(rec.t, ray->direction));
         rec.front = dot3(ray->direction, rec.normal) < 0.0f;
@@ -463,6 +471,8 @@ int oracle_render(const wcpt_scene_data* sd, const wcpt_material* materials, con
         sum.triangle_tests += jobs[t].cnt.triangle_tests;
         sum.hits += jobs[t].cnt.hits;
         sum.draw_fetches += jobs[t].cnt.draw_fetches;
+        sum.ref_stack_overflow_segments += jobs[t].cnt.ref_stack_overflow_segments;
+        if (jobs[t].cnt.ref_stack_max > sum.ref_stack_max) sum.ref_stack_max = jobs[t].cnt.ref_stack_max;
         if (jobs[t].overflow) rc = WCPT_ERROR_STACK_OVERFLOW;
     }
     if (out) *out = sum;

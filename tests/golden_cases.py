@@ -7,4 +7,8 @@ CASES = {
     "cornell_c1_256": ("cornell", 256, 256, 1, 1, (0,)),      # BASELINE config 1
     "cornell_64_b4": ("cornell", 64, 64, 4, 1, (0, 1)),
     "atrium_64x36_b4": ("atrium", 64, 36, 4, 1, (0,)),
+    # the reference's own Init scene (mushroom.obj + 4 spheres, start camera; PathTracingRenderer.jai:219-343) with its
+    # default knobs (maxBounceCount 3, samples 1, :119-120) and the editor's still-camera frame sequence 1, 3
+    "reference_init_64x36": ("reference_init", 64, 36, 3, 1, (1, 3)),
+    "reference_init_glass_64x36_2spp": ("reference_init_glass", 64, 36, 3, 2, (0,)),
 }

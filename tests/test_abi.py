@@ -29,7 +29,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert wcpt.lib.wcpt_abi_version() == 1
+    assert wcpt.lib.wcpt_abi_version() == wcpt._lib.ABI_VERSION == 2
 
 
 def test_option_and_kernel_constants_match_header():
@@ -71,6 +71,9 @@ _Static_assert(offsetof(wcpt_material, ior) == 56, "ior");
 _Static_assert(sizeof(wcpt_sphere) == 20, "Sphere");
 _Static_assert(sizeof(wcpt_node) == 32, "Node");
 _Static_assert(sizeof(wcpt_draw_command) == 32, "DrawCommand");
+_Static_assert(sizeof(wcpt_counters) == 16 * 8, "counters (ABI 2)");
+_Static_assert(offsetof(wcpt_counters, ref_stack_overflow_segments) == 14 * 8, "reference-stack fields last");
+_Static_assert(WCPT_PAYLOAD_RGB32F == 3 && WCPT_PAYLOAD_RGBA32F == 4 && WCPT_PAYLOAD_DISPLAY_RGBA8 == 8, "payloads");
 int main(void) {{ return 0; }}
 ''')
     rc = os.system(f"gcc -std=c99 -Wall -Werror -c {src} -o {tmp_path / 't.o'}")
@@ -106,3 +109,35 @@ def test_python_package_fails_loudly_without_library(tmp_path):
     shutil.copytree(os.path.join(ROOT, "wc-path-tracer_amd", "wcpt"), pkg / "wcpt")
     r = subprocess.run([sys.executable, "-c", "import wcpt"], cwd=pkg, capture_output=True, text=True)
     assert r.returncode != 0 and "libwcpt.so not found" in r.stderr
+
+
+def test_counters_struct_matches_header():
+    assert C.sizeof(wcpt._lib.Counters) == 128
+    assert wcpt._lib.Counters.ref_stack_overflow_segments.offset == 14 * 8
+    assert wcpt.COUNTER_FIELDS[-2:] == ("ref_stack_overflow_segments", "ref_stack_max")
+
+
+def test_group_entry_points_reject_bad_arguments():
+    """wcpt_group_*: argument checks come before any device work, and nothing aborts without a device."""
+    lib = wcpt.lib
+    h = C.c_void_p()
+    devs = (C.c_int * 2)(0, 1)
+    assert lib.wcpt_group_create(devs, 2, 0, None) == -1000
+    assert lib.wcpt_group_create(None, 1, 0, C.byref(h)) == -1000
+    assert lib.wcpt_group_create(devs, 0, 0, C.byref(h)) == -1000
+    assert lib.wcpt_group_create(devs, 2, 2, C.byref(h)) == -1000     # root outside the group
+    assert lib.wcpt_group_destroy(None) == 0
+    assert lib.wcpt_group_context(None, 0) is None
+    assert lib.wcpt_group_create_screen(None, 8, 8) == -1001
+    assert lib.wcpt_group_set_output(None, 4, 0, 0) == -1001
+    assert lib.wcpt_group_sync(None) == -1001
+    if wcpt.device_count() == 0:
+        assert lib.wcpt_group_create(devs, 1, 0, C.byref(h)) == -3     # WCPT_ERROR_INITIALIZATION_FAILED
+        assert not h.value
+        with pytest.raises(wcpt.WcptError):
+            wcpt.Group([0])
+
+
+def test_runtime_version_reported():
+    v = wcpt.runtime_version()
+    assert v >= 70000000, v   # ROCm 7.x HIP runtime (hipRuntimeGetVersion works without a device)

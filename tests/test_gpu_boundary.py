@@ -126,10 +126,15 @@ def test_index_count_past_index_buffer_is_rejected(gpu_ctx):
         dev.free()
 
 
-@pytest.mark.parametrize("pairs", [0, 1])
-def test_vertex_index_past_vertex_buffer_never_hits(gpu_ctx, pairs):
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+@pytest.mark.parametrize("path", ["singles", "pairs", "index"])
+def test_vertex_index_past_vertex_buffer_never_hits(gpu_ctx, kernel, path):
     """An index past the vertex buffer (undefined in the reference) gives a triangle no ray accepts: the frame equals
-    the oracle's frame in which that triangle's vertex is NaN."""
+    the oracle's frame in which that triangle's vertex is NaN. Through the derived records (single and pair records;
+    the one leaf ends at the draw's last triangle) and through the index path (the draw's indexCount covers only the
+    first triangle, so the leaf is not record-backed and its triangles are gathered from the index and vertex
+    buffers, pt_device.h tri_from_indices), in both kernels."""
+    pairs = {"singles": 0, "pairs": 1, "index": -1}[path]
     rng = np.random.default_rng(11)
     ntri = 24
     pos = (rng.random((ntri * 3, 3), dtype=np.float32) * 2.0 - 1.0).astype(np.float32)
@@ -144,7 +149,13 @@ def test_vertex_index_past_vertex_buffer_never_hits(gpu_ctx, pairs):
     s = _with_mesh(get_scene("default"), wscene.HostBVH(pos, idx_dev, nodes))
     dev = wcpt.DeviceScene(gpu_ctx, s)
     gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, pairs)
+    gpu_ctx.set_kernel(kernel)
     try:
+        if path == "index":
+            draws = np.zeros(1, dtype=wcpt._lib.DRAW_COMMAND_DTYPE)
+            draws[0] = (gpu_ctx.buffer_address(dev.buffers[2]), gpu_ctx.buffer_address(dev.buffers[3]),
+                        gpu_ctx.buffer_address(dev.buffers[4]), 3, 0)
+            gpu_ctx.buffer_upload(dev.buffers[5], draws)
         W, H = 48, 40
         gpu_ctx.create_screen(W, H)
         sd = s.scene_data(W, H, max_bounce=2)
@@ -161,6 +172,7 @@ def test_vertex_index_past_vertex_buffer_never_hits(gpu_ctx, pairs):
         assert (full != ref).any(), "the test triangle must be visible"
     finally:
         gpu_ctx.set_option(wcpt._lib.OPTION_PAIR_RECORDS, -1)
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
         dev.free()
 
 

@@ -183,6 +183,8 @@ def test_device_random_direction(gpu_ctx):
     ("cornell", 128, 96, 4, 1),
     ("cornell", 67, 45, 4, 3),          # ragged: not a multiple of the 8x8 tile
     ("atrium", 96, 54, 4, 1),
+    ("reference_init", 96, 54, 3, 1),        # the reference's own Init scene (mushroom.obj), start camera
+    ("reference_init_glass", 96, 54, 3, 2),  # ... with material 0 made DIELECTRIC (Appendix A item 2)
 ])
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_frame_parity(gpu_ctx, name, W, H, bounces, spp, kernel):
@@ -426,7 +428,7 @@ def test_record_formats_match_oracle(gpu_ctx, pairs, name, W, H):
 def test_multi_draw_deep_trees_match_oracle(gpu_ctx, kernel, pairs, combo):
     """Several draw commands over deep BVHs (:151-201: the next draw's traversal starts with the stack of the previous
     one exhausted, closest hit over all of them, ties to the earlier draw). The megakernel walks multiple draws in
-    one flat traversal loop; the atrium's 33-level midpoint tree drives its stacks into the scratch spill."""
+    one flat traversal loop; the atrium's 27-level midpoint tree drives its stacks into the scratch spill."""
     import copy
     s = copy.copy(get_scene("atrium"))
     atrium = s.meshes[0]
@@ -841,17 +843,18 @@ def test_wavefront_pipelines_full_frame(gpu_ctx):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("channels", [3, 4])
+@pytest.mark.parametrize("channels", [3, 4, 8])
 def test_gather_output_equals_image(gpu_ctx, kernel, channels):
-    """wcpt_set_gather_output: the render writes each pixel of its row block into the payload buffer too (RGB or
-    RGBA), bit-identical to the accumulation image, including progressive frames and a row block."""
+    """wcpt_set_gather_output: the render writes each pixel of its row block into the payload buffer too: RGB or
+    RGBA bit-identical to the accumulation image, or (8 = WCPT_PAYLOAD_DISPLAY_RGBA8) composite.comp's display value
+    as RGBA8, bit-identical to the oracle's composite of the accumulated frame -- progressive frames, a row block."""
     s = get_scene("cornell")
     W, H = 96, 80
     y0, rows = row_block(H, 3, 1)
     dev = wcpt.DeviceScene(gpu_ctx, s)
     gpu_ctx.set_kernel(kernel)
-    nbytes = rows * W * channels * 4
-    buf = gpu_ctx.buffer_from(np.full(rows * W * channels, -7.0, np.float32))
+    nbytes = rows * W * wcpt._lib.PAYLOAD_PIXEL_BYTES[channels]
+    buf = gpu_ctx.buffer_from(np.full(nbytes // 4, -7.0, np.float32))
     try:
         gpu_ctx.create_screen(W, H)
         gpu_ctx.set_row_range(y0, rows)
@@ -862,6 +865,10 @@ def test_gather_output_equals_image(gpu_ctx, kernel, channels):
             gpu_ctx.render(s.scene_data(W, H, max_bounce=4, frame=frame), *dev.addresses())
             gpu_ctx.sync()
             img = gpu_ctx.readback(rows)
+            if channels == wcpt._lib.PAYLOAD_DISPLAY_RGBA8:
+                got8 = np.frombuffer(gpu_ctx.buffer_download(buf, nbytes), np.uint8).reshape(rows, W, 4)
+                assert np.array_equal(got8, oracle.composite(img)[1])
+                continue
             got = np.frombuffer(gpu_ctx.buffer_download(buf, nbytes), np.float32).reshape(rows, W, channels)
             assert np.array_equal(got.view(np.uint32), img[..., :channels].view(np.uint32))
         # too small for the row block -> error, no launch
@@ -874,3 +881,115 @@ def test_gather_output_equals_image(gpu_ctx, kernel, channels):
         gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
         gpu_ctx.buffer_free(buf)
         dev.free()
+
+
+def test_vector_scalar_division_within_1_5_ulp(gpu_ctx):
+    """GLSL vector / scalar (normalize, the sphere normal :145, target.xyz / target.w :301, result / samples :312) is
+    defined in both the kernel and the oracle as v * RN(1/s) (pt_device.h operator/, oracle/pt_oracle.c div3s), one
+    correctly rounded reciprocal and a multiply. Vulkan allows 2.5 ULP for GLSL division; this bounds the kernel's
+    form against the exact quotient at 1.5 ULP (and so within 2 ULP of the correctly rounded quotient), so a drift of
+    the definition on either side shows up here. Parity for those expressions is defined by this form."""
+    rng = np.random.default_rng(16)
+    n = 200000
+    a = (rng.standard_normal(n) * 10.0 ** rng.uniform(-20, 20, n)).astype(np.float32)
+    b = (rng.standard_normal(n) * 10.0 ** rng.uniform(-20, 20, n)).astype(np.float32)
+    a[:6] = [1.0, 3.0, 1e-3, 7.0, -2.5, 0.1]
+    b[:6] = [3.0, 7.0, 3.0, 1e30, 1.0, 0.3]
+    got = gpu_ctx.selftest(16, a.view(np.uint32), b.view(np.uint32)).view(np.float32)
+    with np.errstate(all="ignore"):
+        form = (a * (np.float32(1.0) / b)).astype(np.float32)     # the oracle's div3s in numpy binary32
+        exact = a.astype(np.float64) / b.astype(np.float64)
+    assert np.array_equal(got.view(np.uint32), form.view(np.uint32))
+    ok = np.isfinite(exact) & (np.abs(exact) > 1e-36) & (np.abs(exact) < 1e36)
+    ulp = np.spacing(np.abs(exact[ok]).astype(np.float32)).astype(np.float64)
+    err = np.abs(got[ok].astype(np.float64) - exact[ok]) / ulp
+    assert ok.sum() > n * 0.9
+    assert err.max() <= 1.5, f"max error {err.max():.3f} ULP"
+    rn = exact[ok].astype(np.float32)
+    assert np.abs(got[ok].view(np.int32).astype(np.int64) - rn.view(np.int32).astype(np.int64)).max() <= 2
+
+
+
+# ---- the headline configs at full size (BASELINE.json configs 3-4, and the reference's own scene) -----------------
+def _oracle_bands(s, W, H, bounces, spp, frames, bands, rows):
+    """Oracle renders of row bands [y0, y0 + rows) of the progressive frames `frames` (accumulated in order)."""
+    out = {}
+    for y0 in bands:
+        acc = None
+        cnt = None
+        for f in frames:
+            acc, cnt = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=f, y0=y0, rows=rows,
+                                           image=acc, threads=16)
+        out[y0] = (acc, cnt)
+    return out
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_c3_full_frame_vs_oracle(gpu_ctx, kernel):
+    """BASELINE config 3 (the 262k-triangle atrium, 1920x1080, 1 spp, 4 bounces) on both kernels -- the wavefront one
+    is the headline c3 kernel -- against the oracle over the WHOLE frame: image bit-exact and every work counter
+    equal (the reference's stack stays within its 32 entries: ref_stack_max <= 32, no overflowing segment)."""
+    s = get_scene("atrium")
+    W, H = 1920, 1080
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=4, frame=0, kernel=kernel)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=4, frame=0, threads=16)
+    assert_close(img, ref)
+    assert cnt == rcnt
+    assert rcnt["ref_stack_overflow_segments"] == 0 and rcnt["ref_stack_max"] <= 32
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_c4_bands_vs_oracle(gpu_ctx, kernel):
+    """BASELINE config 4 (atrium, 3840x2160, 16 spp in one dispatch, 4 bounces: samples * (maxBounceCount + 1) = 80
+    trace/shade iterations per wavefront pipeline) rendered as the 270-row blocks of the 8-GPU split: the top block,
+    the block starting at row 1080 (a block boundary) and the bottom block, progressive frames 0 and 1, against the
+    oracle on 8-row bands at the top, the boundary and the bottom of those blocks, with exact counters per band."""
+    s = get_scene("atrium")
+    W, H, spp, bounces = 3840, 2160, 16, 4
+    bands = {0: 0, 1080: 1080, 2160 - 270: 2160 - 8}      # block y0 -> band y0 inside it
+    for by0, band in bands.items():
+        dev = wcpt.DeviceScene(gpu_ctx, s)
+        gpu_ctx.set_kernel(kernel)
+        try:
+            gpu_ctx.create_screen(W, H)
+            gpu_ctx.set_row_range(by0, 270)
+            for f in (0, 1):
+                gpu_ctx.render(s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f), *dev.addresses())
+            gpu_ctx.sync()
+            blk = gpu_ctx.readback(270)
+            gpu_ctx.set_row_range(band, 8)
+            cnt = gpu_ctx.render_counters(s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=1),
+                                          *dev.addresses())
+        finally:
+            gpu_ctx.set_row_range(0, 0)
+            gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+            dev.free()
+        ref, rcnt = _oracle_bands(s, W, H, bounces, spp, (0, 1), [band], 8)[band]
+        assert_close(blk[band - by0:band - by0 + 8], ref)
+        assert cnt == rcnt
+        assert rcnt["ref_stack_overflow_segments"] == 0
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name", ["reference_init", "reference_init_glass"])
+def test_reference_init_full_size_rows(gpu_ctx, kernel, name):
+    """The reference's own scene at the headline size (1920x1080, its default maxBounceCount 3 and 1 spp, the editor's
+    still-camera frames 1 then 3): oracle row bands, bit-exact, counters exact."""
+    s = get_scene(name)
+    W, H = 1920, 1080
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    gpu_ctx.set_kernel(kernel)
+    try:
+        gpu_ctx.create_screen(W, H)
+        for f in (1, 3):
+            gpu_ctx.render(s.scene_data(W, H, max_bounce=3, frame=f), *dev.addresses())
+        gpu_ctx.sync()
+        img = gpu_ctx.readback(H)
+        cnt = gpu_ctx.render_counters(s.scene_data(W, H, max_bounce=3, frame=3), *dev.addresses())
+    finally:
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        dev.free()
+    for y0, (ref, _) in _oracle_bands(s, W, H, 3, 1, (1, 3), (0, 270, 536, 1072), 8).items():
+        assert_close(img[y0:y0 + 8], ref)
+    _, rcnt = oracle.render_scene(s, W, H, max_bounce=3, frame=3, threads=16)
+    assert cnt == rcnt

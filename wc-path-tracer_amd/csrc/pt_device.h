@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "../../include/wcpt.h"
+#include "wcpt_composite.h"
 #include "wcpt_libm.h"
 
 namespace wcpt {
@@ -462,11 +463,16 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { r
  * The reference's BVH keeps each leaf's index triples contiguous (PathTracingRenderer.jai:233), so a leaf's
  * records are contiguous. A leaf whose first index position is not a multiple of 3 (never produced by the
  * reference's builder) or that reaches past the draw's indexCount uses the index path.
- * Per-draw table entry: {single record address, pair record address, triangle count, flags, primary-ray pair record
- * address or 0} (5 x u64). */
+ * Per-draw table entry: {single record address, pair record address, triangle count, flags | vertex count << 32,
+ * primary-ray pair record address or 0} (5 x u64). */
 constexpr uint32_t kTriTableWords = 5;
 constexpr uint64_t kTriFlagPackedRefs = 1u; /* table word 3: stack entries may carry (left, count) */
 constexpr uint64_t kTriFlagIndex24 = 2u;    /* table word 3: the draw's indexCount is < 2^24 */
+/* table word 3, bits 32..63: vertices in the draw's vertex buffer (0xFFFFFFFF: unknown, not a context buffer) */
+__device__ __forceinline__ uint32_t draw_vertex_count(const uint64_t* __restrict__ tri_records, uint32_t draw)
+{
+    return (uint32_t)(tri_records[kTriTableWords * draw + 3u] >> 32);
+}
 typedef const WCPT_GLOBAL v4f* gtri_ptr;
 struct TriE { f3 a, e1, e2; };
 __device__ __forceinline__ TriE load_tri(gtri_ptr t, uint32_t k)
@@ -639,11 +645,20 @@ __device__ __forceinline__ void primary_terms(float ox, float oy, float oz, floa
     out[6] = (e2x * qx + e2y * qy) + e2z * qz;
 }
 
-__device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first)
+/* Vertex i of a draw whose vertex buffer holds nvert vertices (table word 3, high half; 0xFFFFFFFF when the buffer
+ * is not a context buffer): a vertex index past the buffer reads NaN instead of memory past it, so that triangle is
+ * never accepted (every comparison with NaN fails) -- the same rule the derived records follow (tri_fields). */
+__device__ __forceinline__ f3 ld_vertex(gf32_ptr vtx, uint32_t i, uint32_t nvert)
 {
-    const f3 a = ld3(vtx + 3ull * idx[first + 0]);
-    const f3 b = ld3(vtx + 3ull * idx[first + 1]);
-    const f3 c = ld3(vtx + 3ull * idx[first + 2]);
+    if (__builtin_expect(i < nvert, 1)) return ld3(vtx + 3ull * i);
+    const float qnan = __uint_as_float(0x7fc00000u);
+    return mk3(qnan, qnan, qnan);
+}
+__device__ __forceinline__ TriE tri_from_indices(gu32_ptr idx, gf32_ptr vtx, uint32_t first, uint32_t nvert)
+{
+    const f3 a = ld_vertex(vtx, idx[first + 0], nvert);
+    const f3 b = ld_vertex(vtx, idx[first + 1], nvert);
+    const f3 c = ld_vertex(vtx, idx[first + 2], nvert);
     TriE e;
     e.a = a;
     e.e1 = b - a;
@@ -663,12 +678,14 @@ __device__ __forceinline__ uint32_t leaf_record(uint32_t first, uint32_t count, 
  * leaf's first record is at 16 * first), without a division: for first < 2^24 (draws with kTriFlagIndex24),
  * first % 3 == 0 exactly when (first * 0xAAAAAB) mod 2^24 <= 0x555555 (0xAAAAAB is the inverse of 3 mod 2^24; checked
  * for every first < 2^24), one full-rate v_mul_u32_u24 instead of leaf_record's quarter-rate v_mul_hi_u32 pair.
- * The end test first + count + 2 <= 3 * ntri is leaf_record's for counts that are multiples of 3 (the reference's)
- * and at most stricter otherwise (such a leaf takes the index path). lim3 = 3 * ntri. */
+ * The end test is leaf_record's k + ceil(count / 3) <= ntri for every count: with first = 3k and lim3 = 3 * ntri,
+ * lim3 - first is a multiple of 3, and count <= M holds for a multiple M of 3 exactly when 3 * ceil(count / 3) <= M.
+ * It is written as first <= lim3 && count <= lim3 - first, which cannot wrap; lim3 < 2^24 for these draws, so an
+ * accepted first is < 2^24 and the 24-bit alignment test above is exact for it. */
 __device__ __forceinline__ uint32_t leaf_record_off24(uint32_t first, uint32_t count, uint32_t lim3)
 {
     const bool aligned = (__umul24(first, 0xAAAAABu) & 0xFFFFFFu) <= 0x555555u;
-    return (aligned && first + count + 2u <= lim3) ? first * 16u : kNoRecord;
+    return (aligned && first <= lim3 && count <= lim3 - first) ? first * 16u : kNoRecord;
 }
 /* leaf_record as a byte offset for any draw (records beyond 4 GiB take the index path) */
 __device__ __forceinline__ uint32_t leaf_record_off(uint32_t first, uint32_t count, uint32_t ntri)
@@ -719,10 +736,72 @@ __device__ __forceinline__ void sink_u(uint32_t x) { asm volatile("" ::"v"(x)); 
 struct Counters {
     uint32_t pixels, segments, sphere_tests, node_pops, interior_visits, triangle_tests, hits, draw_fetches;
     uint32_t wave_int, lane_int, wave_tri, lane_tri, wave_seg, lane_seg; /* SIMD-efficiency diagnostics */
+    uint32_t ref_over;  /* segments whose reference stack (uint nodeStack[32], :151) is written past index 31 */
+    uint32_t ref_max;   /* deepest reference stack (entries after a push), 0xFFFFFFFF when it could not be tracked */
+    bool ref_seg;       /* the current segment overflowed the reference stack */
 #if WCPT_MK_TIMERS
     uint64_t tim[kPhaseTimers], tprev;
 #endif
 };
+
+/* The reference's traversal stack, tracked exactly in the counting builds.
+ * pathTracer.comp pushes the root (:155) and, at every interior node that survives its box test, BOTH children
+ * (:192-198), culling a child only when it is popped (:162). So while a node is visited, its stack index (the entries
+ * below it) is the number of its ancestors whose second-popped child is still pending -- the ancestors where the walk
+ * went into the first-popped ("near") child. The kernels push only far children that pass their box test, so this
+ * index is kept as two path masks instead of a second stack: bit k of `near` = the ancestor at depth k was left
+ * through its near child (its far child is still pending in the reference), bit k of `pushed` = that far child is on
+ * this kernel's stack. An interior visit pushes at indices rs and rs + 1 with rs = popcount(near); rs >= 31 writes
+ * nodeStack[32], out of bounds (undefined behaviour in the reference). A pop of this kernel's stack takes the far
+ * child of the deepest `pushed` ancestor k; the reference pops (and culls) every pending entry above it first. */
+struct RefStack {
+    uint64_t nearm, pushed;
+    uint32_t depth;
+};
+constexpr uint32_t kRefStackSize = 32u;  /* uint nodeStack[32] (pathTracer.comp:151) */
+constexpr uint32_t kRefUnknown = 0xFFFFFFFFu;
+template <bool COUNT>
+__device__ __forceinline__ void ref_root(RefStack& r, Counters& cnt)
+{
+    if (!COUNT) return;
+    r.nearm = 0;
+    r.pushed = 0;
+    r.depth = 0;
+    if (cnt.ref_max < 1u) cnt.ref_max = 1u; /* the root push (:155) */
+}
+template <bool COUNT>
+__device__ __forceinline__ void ref_interior(RefStack& r, bool pushed_far, Counters& cnt)
+{
+    if (!COUNT) return;
+    const uint32_t rs = (uint32_t)__popcll(r.nearm);
+    if (rs + 2u > kRefStackSize) cnt.ref_seg = true;
+    if (r.depth < 64u) {
+        if (cnt.ref_max != kRefUnknown && cnt.ref_max < rs + 2u) cnt.ref_max = rs + 2u;
+        const uint64_t b = 1ull << r.depth;
+        r.nearm |= b;
+        if (pushed_far) r.pushed |= b;
+    } else {
+        cnt.ref_max = kRefUnknown; /* deeper than the masks: not tracked */
+    }
+    r.depth++;
+}
+template <bool COUNT>
+__device__ __forceinline__ void ref_pop(RefStack& r)
+{
+    if (!COUNT || r.pushed == 0) return;
+    const uint32_t k = 63u - (uint32_t)__clzll((long long)r.pushed);
+    const uint64_t below = (1ull << k) - 1ull;
+    r.nearm &= below;
+    r.pushed &= below;
+    r.depth = k + 1u;
+}
+template <bool COUNT>
+__device__ __forceinline__ void ref_segment_end(Counters& cnt)
+{
+    if (!COUNT) return;
+    if (cnt.ref_seg) cnt.ref_over++;
+    cnt.ref_seg = false;
+}
 
 __device__ __forceinline__ void phase_start(Counters& c)
 {
@@ -851,12 +930,9 @@ __device__ __forceinline__ f3 triangle_normal(uint32_t prim, uint32_t draw, cons
         const v4f r2 = t[3ull * k + 2u];
         return mk3(r2.y, r2.z, r2.w);
     }
-    const gu32_ptr idx = as_u32(draws[draw].indexBuffer);
-    const gf32_ptr vtx = as_f32(draws[draw].vertexBuffer);
-    const f3 a = ld3(vtx + 3ull * idx[prim + 0]);
-    const f3 b = ld3(vtx + 3ull * idx[prim + 1]);
-    const f3 c = ld3(vtx + 3ull * idx[prim + 2]);
-    return normalize(cross(b - a, c - a));
+    const TriE e = tri_from_indices(as_u32(draws[draw].indexBuffer), as_f32(draws[draw].vertexBuffer), prim,
+                                    tri_records ? draw_vertex_count(tri_records, draw) : 0xFFFFFFFFu);
+    return normalize(cross(e.e1, e.e2));
 }
 
 /* Intersect epilogue (:204-208) for winner `prim` (kNoPrim, kSpherePrim | sphere, or the index position of
@@ -897,6 +973,7 @@ struct DrawGeom {
     gtri_ptr tris;  /* pair records (PAIRS) or single records */
     gtri_ptr ptris; /* primary-ray pair records (PAIRS, when the runtime built them; table word 4) or null */
     uint32_t ntri;
+    uint32_t nvert; /* vertex count bound of the index path (draw_vertex_count) */
     bool packed; /* stack entries carry (left, count): kTriFlagPackedRefs */
 };
 template <bool PAIRS>
@@ -910,6 +987,7 @@ __device__ __forceinline__ DrawGeom draw_geom(const wcpt_draw_command* __restric
     g.tris = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + (PAIRS ? 1u : 0u)];
     g.ptris = PAIRS ? (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * i + 4u] : nullptr;
     g.ntri = (uint32_t)tri_records[kTriTableWords * i + 2u];
+    g.nvert = draw_vertex_count(tri_records, i);
     g.packed = (tri_records[kTriTableWords * i + 3u] & kTriFlagPackedRefs) != 0u;
     return g;
 }
@@ -1057,7 +1135,7 @@ __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uin
         for (uint32_t k = 0, j = 0; k < curCount; k += 3, j++) {
             const uint32_t first = k + curLeft;
             const TriE tr = (!PAIRS && k0 != kNoRecord) ? load_tri(g.tris, k0 + j)
-                                                        : tri_from_indices(g.indices, g.vertices, first);
+                                                        : tri_from_indices(g.indices, g.vertices, first, g.nvert);
             const float t = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
             count_tri<COUNT, DIAG>(cnt);
             if (t != -1.0f && t < rt) {
@@ -1073,7 +1151,8 @@ __device__ __forceinline__ void leaf_step(const Ray& ray, const DrawGeom& g, uin
  * passes, and return true with the cursor on the nearer child if that one passes and is not culled by rec.t. */
 template <bool COUNT, bool DIAG, class Stack>
 __device__ __forceinline__ bool interior_step(const Ray& ray, const DrawGeom& g, Stack& stk, uint32_t& curLeft,
-                                              uint32_t& curCount, float rt, Counters& cnt, bool& overflow)
+                                              uint32_t& curCount, float rt, Counters& cnt, bool& overflow,
+                                              RefStack& rf)
 {
     const NodeV L = load_node(g.bvh, curLeft);
     const NodeV R = load_node(g.bvh, curLeft + 1);
@@ -1110,6 +1189,7 @@ __device__ __forceinline__ bool interior_step(const Ray& ray, const DrawGeom& g,
     const float farT0 = leftFirst ? r0 : l0;
     const NodeV& F = leftFirst ? R : L;
     if (passFar && !stk.push(node_ref(g.packed, farIdx, F.b.z, F.b.w), farT0)) overflow = true;
+    ref_interior<COUNT>(rf, passFar, cnt);
     phase_mark(cnt, 2);
     if (passNear && !(nearT0 > rt)) {
         const NodeV& N = leftFirst ? L : R;
@@ -1121,15 +1201,16 @@ __device__ __forceinline__ bool interior_step(const Ray& ray, const DrawGeom& g,
 }
 
 /* Pop (:157-162): the next deferred node whose box entry distance is not beyond rec.t; false when none is left. */
-template <class Stack>
+template <bool COUNT, class Stack>
 __device__ __forceinline__ bool pop_step(const DrawGeom& g, Stack& stk, uint32_t& curLeft, uint32_t& curCount, float rt,
-                                         Counters& cnt)
+                                         Counters& cnt, RefStack& rf)
 {
     bool found = false;
     while (!stk.empty()) {
         uint32_t ni;
         float t0;
         stk.pop(ni, t0);
+        ref_pop<COUNT>(rf);
         if (t0 > rt) continue;
         const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
         curLeft = lc.x;
@@ -1145,9 +1226,10 @@ __device__ __forceinline__ bool pop_step(const DrawGeom& g, Stack& stk, uint32_t
  * survives the cull. */
 template <bool COUNT>
 __device__ __forceinline__ bool root_step(const Ray& ray, const DrawGeom& g, float rt, uint32_t& curLeft,
-                                          uint32_t& curCount, Counters& cnt)
+                                          uint32_t& curCount, Counters& cnt, RefStack& rf)
 {
     if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
+    ref_root<COUNT>(rf, cnt);
     const NodeV cur = load_node(g.bvh, 0);
     float c0, c1;
     node_box(ray, cur, c0, c1);
@@ -1202,6 +1284,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     PeelCache pc;
     pc.tag = kNoPeel;
     pc.t = bc2(0.0f);
+    RefStack rf;
     if constexpr (SINGLE) {
         const DrawGeom g = draw_geom<PAIRS>(draws, tri_records, 0);
         /* one traversal step per iteration as sequential ifs on the lane's mode (pop -> interior -> leaf), like
@@ -1209,15 +1292,16 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
          * leaf tests it in the same iteration */
         enum : uint32_t { kInterior = 0, kLeaf = 1, kPop = 2, kDone = 3 };
         uint32_t mode = kDone;
-        if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
+        if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt, rf)) {
             stk.reset();
             mode = curCount > 0 ? kLeaf : kInterior;
         }
         while (mode != kDone) {
             if (mode == kPop)
-                mode = pop_step(g, stk, curLeft, curCount, rt, cnt) ? (curCount > 0 ? kLeaf : kInterior) : kDone;
+                mode = pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf) ? (curCount > 0 ? kLeaf : kInterior)
+                                                                                : kDone;
             if (mode == kInterior)
-                mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)
+                mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)
                            ? (curCount > 0 ? kLeaf : kInterior) : kPop;
             if (mode == kLeaf) {
                 leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
@@ -1233,7 +1317,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
             for (; d < sd.drawCommandCount; d++) {
                 g = draw_geom<PAIRS>(draws, tri_records, d);
                 rt_before = rt;
-                if (root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt)) {
+                if (root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt, rf)) {
                     stk.reset();
                     pc.tag = kNoPeel; /* offsets of another draw's records */
                     return true;
@@ -1245,10 +1329,10 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
         while (active) {
             if (curCount > 0) {
                 leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
-            } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow)) {
+            } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)) {
                 continue;
             }
-            if (pop_step(g, stk, curLeft, curCount, rt, cnt)) continue;
+            if (pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf)) continue;
             if (rt != rt_before) primDraw = d; /* this draw lowered rt: it owns prim */
             d++;
             active = start_draw();
@@ -1256,6 +1340,7 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
     }
 
     if (COUNT && prim != kNoPrim) cnt.hits++;
+    ref_segment_end<COUNT>(cnt);
     const Hit hit = resolve_hit(ray, rt, prim, primDraw, spheres, draws, tri_records);
     phase_mark(cnt, 4);
     return hit;
@@ -1464,7 +1549,18 @@ __device__ __forceinline__ f3 primary_direction(const wcpt_scene_data& sd, uint3
 }
 
 /* Final store of a pixel (pathTracer.comp:323, `vec4(acc, 1)`): the accumulation image, plus the gather payload
- * (wcpt_set_gather_output) when the host asked for one -- RGB (3 floats) or RGBA, same row-major pixel index. */
+ * (wcpt_set_gather_output) when the host asked for one, same row-major pixel index: RGB (3 floats), RGBA (4 floats),
+ * or WCPT_PAYLOAD_DISPLAY_RGBA8 -- the display step of composite.comp:36-53 (gamma 1/2.2 + PBR Neutral, then UNORM8)
+ * applied to the accumulated value as it is stored, so a multi-device frame travels at 4 B/px
+ * with no composite pass over the image. */
+__device__ __noinline__ uint32_t display_rgba8(f3 acc)
+{
+    const float in[4] = {acc.x, acc.y, acc.z, 1.0f};
+    float o[4];
+    wcpt_composite_texel(in, o);
+    return (uint32_t)wcpt_unorm8(o[0]) | ((uint32_t)wcpt_unorm8(o[1]) << 8) | ((uint32_t)wcpt_unorm8(o[2]) << 16) |
+           (255u << 24);
+}
 __device__ __forceinline__ void store_pixel(float4* __restrict__ image, float* __restrict__ wire, uint32_t wire_ch,
                                             size_t i, f3 acc)
 {
@@ -1475,8 +1571,10 @@ __device__ __forceinline__ void store_pixel(float4* __restrict__ image, float* _
             w[0] = acc.x;
             w[1] = acc.y;
             w[2] = acc.z;
-        } else {
+        } else if (wire_ch == 4u) {
             reinterpret_cast<float4*>(wire)[i] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        } else {
+            reinterpret_cast<uint32_t*>(wire)[i] = display_rgba8(acc);
         }
     }
 }
@@ -1490,8 +1588,8 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint32_t v
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
 }
 
-/* Wave-reduce the per-lane counters into the 14 global u64 counters (wcpt_counters order). All 64 lanes of
- * the wave must call it. */
+/* Wave-reduce the per-lane counters into the 16 global u64 counters (wcpt_counters order; the last is a maximum).
+ * All 64 lanes of the wave must call it. */
 template <bool COUNT>
 __device__ __forceinline__ void flush_counters(const Counters& cnt, unsigned long long* __restrict__ counters)
 {
@@ -1510,6 +1608,11 @@ __device__ __forceinline__ void flush_counters(const Counters& cnt, unsigned lon
         wave_add_u64(&counters[11], cnt.lane_tri);
         wave_add_u64(&counters[12], cnt.wave_seg);
         wave_add_u64(&counters[13], cnt.lane_seg);
+        wave_add_u64(&counters[14], cnt.ref_over);
+        uint32_t m = cnt.ref_max;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        if ((threadIdx.x & 63) == 0 && m) atomicMax(&counters[15], (unsigned long long)m);
     }
 }
 

@@ -135,6 +135,10 @@ void wf_release(WfPipes& w);
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n,
                            hipStream_t stream);
 
+/* wcpt_runtime.hip internals used by the multi-device group (wcpt_group.hip) */
+hipStream_t context_stream(wcpt_context* ctx);
+int context_error(wcpt_context* ctx, int code, const char* msg);
+
 } // namespace wcpt
 
 #endif

@@ -300,6 +300,11 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
         out[i] = bad;
         break;
     }
+    case 16: { /* GLSL vector / scalar as the kernels evaluate it (pt_device.h operator/): in * RN(1 / in2) */
+        const f3 q = mk3(__uint_as_float(a), 0.0f, 0.0f) / __uint_as_float(in2[i]);
+        out[i] = __float_as_uint(q.x);
+        break;
+    }
     case 7: { /* RandomDirection: 3 words per input */
         uint32_t s = a;
         const f3 d = RandomDirection(s);

@@ -257,6 +257,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     uint32_t ca = 0, cb = 0, cr = 0, mode = kModeDone;
     float rt = kInfinity;
     bool any = false; /* this ray is the last segment of its pixel's last sample (render build only) */
+    RefStack rf;      /* the reference's stack index (counting builds, pt_device.h RefStack) */
     Ray ray;
     uint64_t tim[kDiagTimers] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tprev = DIAG ? __builtin_amdgcn_s_memtime() : 0;
@@ -267,6 +268,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             if (!SINGLE) gl = load_geom(draws, tri_records, d);
             const Geom& g = SINGLE ? g0 : gl;
             if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
+            ref_root<COUNT>(rf, cnt);
             const NodeV root = load_node(g.bvh, 0);
             float c0, c1;
             node_box(ray, root, c0, c1);
@@ -346,6 +348,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     uint32_t ni;
                     float t0;
                     stk.pop(ni, t0);
+                    ref_pop<COUNT>(rf);
                     if (t0 > rt) continue;
                     const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
                     cursor_from(lc.x, lc.y, g, ca, cb, cr, mode);
@@ -385,6 +388,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     if (!stk.push(node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w), farT0))
                         overflow = true;
                 }
+                ref_interior<COUNT>(rf, passFar, cnt); /* the counting build pushes every passing far child */
                 if (passNear && !((leftFirst ? l0 : r0) > rt)) {
                     const uint32_t nl = leftFirst ? L.b.z : R.b.z, nc = leftFirst ? L.b.w : R.b.w;
                     cursor_from(nl, nc, g, ca, cb, cr, mode);
@@ -396,7 +400,9 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             if (has && mode == kModeLeaf) {
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
-                const TriE tr = cr != kNoRecord ? load_tri_at(g.tris, cr) : tri_from_indices(g.indices, g.vertices, ca);
+                const TriE tr = cr != kNoRecord ? load_tri_at(g.tris, cr)
+                                                : tri_from_indices(g.indices, g.vertices, ca,
+                                                                   draw_vertex_count(tri_records, SINGLE ? 0u : d));
                 const float tt = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
                 if (COUNT) {
                     cnt.triangle_tests++;
@@ -417,6 +423,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             if (has && mode == kModeDone) {
                 /* Intersect result; wf_shade rebuilds the winner's normal and material (:204-208) */
                 b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
+                ref_segment_end<COUNT>(cnt);
                 has = false;
             }
             diag_mark<DIAG>(tim, tprev, 4);

@@ -22,7 +22,7 @@
 
 namespace {
 
-constexpr int kNumCounters = 14; /* wcpt_counters: 8 reference counters + 6 diagnostics */
+constexpr int kNumCounters = 16; /* wcpt_counters: 8 reference counters + 6 diagnostics + 2 reference-stack fields */
 std::mutex g_err_mutex;
 std::string g_last_error;
 
@@ -97,6 +97,9 @@ constexpr double kPairMinTrianglesPerLeaf = 4.0;
 constexpr uint64_t kPairMaxTriangles = 1ull << 26;
 /* Primary-ray pair records for the megakernel (pt_device.h WCPT_PRIMARY_PAIRS) */
 constexpr bool kPrimaryPairs = WCPT_PRIMARY_PAIRS != 0;
+
+/* Bytes per pixel of a gather payload format (wcpt.h WCPT_PAYLOAD_*) */
+uint64_t payload_pixel_bytes(uint32_t format) { return format == WCPT_PAYLOAD_DISPLAY_RGBA8 ? 4u : 4ull * format; }
 
 hipError_t skewed_alloc(Buffer& b, uint64_t bytes)
 {
@@ -324,6 +327,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         const uint64_t nodes = bb ? (bb->bytes - o) / sizeof(wcpt_node) : ~0ull;
         uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
         if (dc[d].indexCount < (1u << 24)) flags |= 2u; /* pt_device.h kTriFlagIndex24 */
+        flags |= (uint64_t)nvert << 32;                 /* pt_device.h draw_vertex_count: bounds the index path */
         const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, flags, ctx->tri_table[W * d + 4]};
         for (uint64_t w = 0; w < W; w++) {
             if (ctx->tri_table[W * d + w] != entry[w]) {
@@ -347,7 +351,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         TriRecords& t = ctx->tri[d];
         uint64_t paddr = 0;
         if (want_primary && t.ntri > 0) {
-            const uint64_t npairs = (uint64_t)t.ntri / 2u + 1u;
+            const uint64_t npairs = ((uint64_t)t.ntri + 1u) / 2u; /* the pair records build_tri_records writes */
             const uint64_t bytes = npairs * wcpt::kPrimPairRecordBytes;
             const bool fresh = t.pvalid && t.pbuild == t.build_id && std::memcmp(t.porigin, origin, sizeof(origin)) == 0;
             if (!fresh) {
@@ -420,9 +424,10 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.wire = nullptr;
     a.wire_ch = ctx->wire_ch;
     if (ctx->wire && mode == wcpt::kModeRender) {
-        if ((uint64_t)ctx->width * ctx->rows * ctx->wire_ch * 4ull > ctx->wire_bytes)
-            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%u x %u",
-                             (unsigned long long)ctx->wire_bytes, ctx->width, ctx->rows, ctx->wire_ch);
+        if ((uint64_t)ctx->width * ctx->rows * payload_pixel_bytes(ctx->wire_ch) > ctx->wire_bytes)
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%u x %u B",
+                             (unsigned long long)ctx->wire_bytes, ctx->width, ctx->rows,
+                             (unsigned)payload_pixel_bytes(ctx->wire_ch));
         a.wire = ctx->wire;
     }
     a.W = ctx->width;
@@ -490,9 +495,24 @@ int read_status(wcpt_context* ctx)
 
 } // namespace
 
+/* Internal hooks for the multi-device group (wcpt_group.hip): a context's current stream, and error reporting
+ * through the same last-error strings as the C entry points. */
+namespace wcpt {
+hipStream_t context_stream(wcpt_context* ctx) { return ctx ? ctx->stream : nullptr; }
+int context_error(wcpt_context* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
+} // namespace wcpt
+
 extern "C" {
 
 int wcpt_abi_version(void) { return WCPT_ABI_VERSION; }
+
+int wcpt_runtime_version(int* version)
+{
+    if (!version) return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "null version");
+    hipError_t e = hipRuntimeGetVersion(version);
+    if (e != hipSuccess) return hip_fail(nullptr, e, "hipRuntimeGetVersion");
+    return WCPT_SUCCESS;
+}
 
 const char* wcpt_last_error(const wcpt_context* ctx)
 {
@@ -827,12 +847,12 @@ int wcpt_set_gather_output(wcpt_context* ctx, uint64_t device_ptr, uint64_t byte
         ctx->wire_bytes = 0;
         return WCPT_SUCCESS;
     }
-    if (channels != 3 && channels != 4)
-        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output channels %u (3 or 4)", channels);
+    if (channels != WCPT_PAYLOAD_RGB32F && channels != WCPT_PAYLOAD_RGBA32F && channels != WCPT_PAYLOAD_DISPLAY_RGBA8)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output format %u (3, 4 or 8)", channels);
     if (bytes == 0 || (device_ptr & 3u))
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output: %llu bytes at a misaligned or empty buffer",
                          (unsigned long long)bytes);
-    if (channels == 4 && (device_ptr & 15u))
+    if (channels == WCPT_PAYLOAD_RGBA32F && (device_ptr & 15u))
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output: RGBA needs 16-byte alignment");
     ctx->wire = reinterpret_cast<float*>(device_ptr);
     ctx->wire_bytes = bytes;
@@ -930,6 +950,8 @@ int wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, uint64
     out->lane_triangle_steps = h[11];
     out->wave_segment_steps = h[12];
     out->lane_segment_steps = h[13];
+    out->ref_stack_overflow_segments = h[14];
+    out->ref_stack_max = h[15] == 0xFFFFFFFFull ? UINT64_MAX : h[15];
     return read_status(ctx);
 }
 
@@ -987,8 +1009,9 @@ int wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const ui
 {
     int rc = bind(ctx);
     if (rc) return rc;
-    if (!in || !out || ((fn == 6 || fn == 14) && !in2)) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
-    if (fn < 0 || fn > 15) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
+    if (!in || !out || ((fn == 6 || fn == 14 || fn == 16) && !in2))
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
+    if (fn < 0 || fn > 16) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
     const uint64_t outw = (fn == 1) ? 4ull * n : (fn == 7 ? 3ull * n : (uint64_t)n);
     rc = ensure_scratch(ctx, (2ull * n + outw) * 4ull + 16);
     if (rc) return rc;

@@ -6,14 +6,15 @@ package is the Python host mirror used by tests and the benchmark.
 from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL,
                    KERNEL_WAVEFRONT, LIB_PATH, MATERIAL_DIELECTRIC, MATERIAL_DTYPE, MATERIAL_METAL, NODE_DTYPE,
                    SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, WcptError, lib)
-from .renderer import Context, DeviceScene, Editor, PathTracingRenderer
+from .renderer import Context, DeviceScene, Editor, Group, PathTracingRenderer
 from . import scene
+from . import _lib
 
 __all__ = [
     "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
-    "PathTracingRenderer", "Editor", "scene", "device_count",
+    "PathTracingRenderer", "Editor", "Group", "scene", "device_count", "runtime_version",
 ]
 
 
@@ -22,3 +23,11 @@ def device_count() -> int:
     n = C.c_int()
     lib.wcpt_device_count(C.byref(n))
     return n.value
+
+
+def runtime_version() -> int:
+    """hipRuntimeGetVersion of the HIP runtime libwcpt.so is bound to (e.g. 70226090 = ROCm 7.2)."""
+    import ctypes as C
+    v = C.c_int()
+    _lib.check(lib.wcpt_runtime_version(C.byref(v)))
+    return v.value

@@ -53,6 +53,12 @@ OPTION_MK_TILE_ORDER = 9
 OPTION_WF_PIPES = 10
 DEFAULT_WF_PIPES = 2  # wcpt_runtime.hip
 
+# gather payload formats (wcpt_set_gather_output, wcpt_group_set_output)
+PAYLOAD_RGB32F = 3
+PAYLOAD_RGBA32F = 4
+PAYLOAD_DISPLAY_RGBA8 = 8
+PAYLOAD_PIXEL_BYTES = {PAYLOAD_RGB32F: 12, PAYLOAD_RGBA32F: 16, PAYLOAD_DISPLAY_RGBA8: 4}
+
 # ---- POD types (byte layouts of include/wcpt.h == the reference's GLSL scalar layouts) -------------------
 SCENE_DATA_DTYPE = np.dtype([
     ("inverseProjection", "<f4", (16,)), ("inverseView", "<f4", (16,)), ("position", "<f4", (3,)),
@@ -67,16 +73,21 @@ NODE_DTYPE = np.dtype([("min", "<f4", (3,)), ("max", "<f4", (3,)), ("leftNodeOrT
                        ("triangleCount", "<u4")])
 DRAW_COMMAND_DTYPE = np.dtype([("vertexBuffer", "<u8"), ("indexBuffer", "<u8"), ("bvhBuffer", "<u8"),
                                ("indexCount", "<u4"), ("_pad", "<u4")])
-COUNTER_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",
-                  "hits", "draw_fetches")
+WORK_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",
+               "hits", "draw_fetches")
 DIAG_FIELDS = ("wave_interior_steps", "lane_interior_steps", "wave_triangle_steps", "lane_triangle_steps",
                "wave_segment_steps", "lane_segment_steps")
+# the reference's uint nodeStack[32] (pathTracer.comp:151): segments that write past it, and its deepest use (a max)
+REF_STACK_FIELDS = ("ref_stack_overflow_segments", "ref_stack_max")
+COUNTER_FIELDS = WORK_FIELDS + REF_STACK_FIELDS
+ABI_VERSION = 2
 assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
 assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
 
 
 class Counters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_FIELDS + DIAG_FIELDS]
+    """wcpt_counters (include/wcpt.h): the 8 work counters, 6 SIMD diagnostics, the 2 reference-stack fields."""
+    _fields_ = [(n, C.c_uint64) for n in WORK_FIELDS + DIAG_FIELDS + REF_STACK_FIELDS]
 
     def as_dict(self, diagnostics: bool = False):
         names = COUNTER_FIELDS + (DIAG_FIELDS if diagnostics else ())
@@ -147,6 +158,14 @@ _PROTOTYPES = {
     "wcpt_mesh_to_obj": (_i, [C.POINTER(Mesh), C.POINTER(C.c_void_p), C.POINTER(_u64)]),
     "wcpt_string_free": (None, [C.c_void_p]),
     "wcpt_selftest_device": (_i, [_p, _i, _p, _p, _p, _u32]),
+    "wcpt_runtime_version": (_i, [C.POINTER(_i)]),
+    "wcpt_group_create": (_i, [C.POINTER(_i), _i, _i, C.POINTER(_p)]),
+    "wcpt_group_destroy": (_i, [_p]),
+    "wcpt_group_context": (_p, [_p, _i]),
+    "wcpt_group_create_screen": (_i, [_p, _u32, _u32]),
+    "wcpt_group_set_output": (_i, [_p, _i, _u64, _u64]),
+    "wcpt_group_render": (_i, [_p, _p, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]),
+    "wcpt_group_sync": (_i, [_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOTYPES)

@@ -19,17 +19,25 @@ from . import scene as _scene
 class Context:
     """One HIP device context (one stream). Not thread-safe, like the reference's single render thread."""
 
-    def __init__(self, device: int = 0):
-        h = C.c_void_p()
-        check(lib.wcpt_create(device, C.byref(h)))
-        self.h = h
+    def __init__(self, device: int = 0, _handle=None):
+        self.owned = _handle is None
+        if _handle is None:
+            h = C.c_void_p()
+            check(lib.wcpt_create(device, C.byref(h)))
+            _handle = h
+        self.h = _handle
         self.device = device
+
+    @classmethod
+    def borrowed(cls, handle, device: int) -> "Context":
+        """A context owned by someone else (a Group's rank context): close() leaves it alone."""
+        return cls(device, _handle=C.c_void_p(handle))
 
     # -- lifetime -----------------------------------------------------------------------------------
     def close(self):
-        if self.h:
+        if self.h and self.owned:
             lib.wcpt_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __enter__(self):
         return self
@@ -108,7 +116,8 @@ class Context:
         self._chk(lib.wcpt_set_external_image(self.h, device_ptr, nbytes))
 
     def set_gather_output(self, device_ptr: int, nbytes: int, channels: int = 3):
-        """The render also writes each pixel into float[rows][width][channels] at device_ptr (0 = off)."""
+        """The render also writes each pixel into its payload at device_ptr (0 = off): channels = 3 / 4 (float RGB /
+        RGBA of the accumulation) or 8 (PAYLOAD_DISPLAY_RGBA8: composite.comp's display value as RGBA8)."""
         self._chk(lib.wcpt_set_gather_output(self.h, device_ptr, nbytes, channels))
 
     def image_ptr(self) -> int:
@@ -200,6 +209,61 @@ class DeviceScene:
         for b in self.buffers:
             self.ctx.buffer_free(b)
         self.buffers = []
+
+
+class Group:
+    """One frame on several devices from one host thread (include/wcpt.h wcpt_group_*): rank r renders
+    rows [r*H/N, (r+1)*H/N) on devices[r], and a set output gathers every frame's blocks to the root over RCCL."""
+
+    def __init__(self, devices, root: int = 0):
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(lib.wcpt_group_create(devs, len(devices), root, C.byref(h)))
+        self.h = h
+        self.devices = list(devices)
+        self.root = root
+        self.contexts = [Context.borrowed(lib.wcpt_group_context(h, r), d) for r, d in enumerate(devices)]
+
+    def close(self):
+        if self.h:
+            for c in self.contexts:
+                c.h = None
+            lib.wcpt_group_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def context(self, rank: int) -> Context:
+        return self.contexts[rank]
+
+    def create_screen(self, width: int, height: int):
+        from .dist import row_block
+        check(lib.wcpt_group_create_screen(self.h, width, height))
+        self.width, self.height = width, height
+        for r, c in enumerate(self.contexts):   # a rank's context holds only its row block
+            c.width, c.height = width, row_block(height, len(self.contexts), r)[1]
+
+    def set_output(self, fmt: int, dst: int, nbytes: int):
+        check(lib.wcpt_group_set_output(self.h, fmt, dst, nbytes))
+
+    def render(self, sd: np.ndarray, materials, spheres, draws):
+        n = len(self.devices)
+        sd = np.ascontiguousarray(sd, dtype=SCENE_DATA_DTYPE)
+        arr = [(C.c_uint64 * n)(*[int(v) for v in a]) for a in (materials, spheres, draws)]
+        check(lib.wcpt_group_render(self.h, ptr(sd), *arr))
+
+    def sync(self):
+        check(lib.wcpt_group_sync(self.h))
 
 
 class PathTracingRenderer:
@@ -336,4 +400,4 @@ class Editor:
         return used
 
 
-__all__ = ["Context", "DeviceScene", "PathTracingRenderer", "Editor", "COUNTER_FIELDS"]
+__all__ = ["Context", "DeviceScene", "Group", "PathTracingRenderer", "Editor", "COUNTER_FIELDS"]

@@ -6,6 +6,7 @@ indices (src/ModelLoader.jai:60-141) -> midpoint BVH with BVH-permuted indices (
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -138,9 +139,43 @@ def make_camera(position=(0.0, 0.0, 0.0), yaw=0.0, pitch=0.0, fov=90.0) -> Camer
     return c
 
 
+ASSETS_DIR = os.environ.get("WCPT_ASSETS", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                          "assets"))
+# The reference's own input: run_tree/data/assets/models/mushroom.obj, loaded by LoadModel
+# (PathTracingRenderer.jai:220); a copy of that mesh data ships with the package.
+MUSHROOM_OBJ = os.path.join(ASSETS_DIR, "mushroom.obj")
+REFERENCE_SCENES = ("reference_init", "reference_init_glass")
+
+
+def reference_init(glass_dielectric: bool = False, obj_path: str | None = None, bvh: str = "midpoint") -> HostScene:
+    """The scene the reference renders after Init (PathTracingRenderer.jai:272-343):
+
+    - LoadModel (:219-243): mushroom.obj through parse_obj_file (ModelLoader.jai:60-141) and the midpoint BVH
+      (:147-217) as one draw command (:251-256);
+    - the 4 materials and 4 spheres of :322-339 (every material METAL: SetDielectric never sets `type`, :78-82; all
+      triangles use material 0, the "glass" one, pathTracer.comp:175);
+    - the editor's start camera (editor.jai:25: a default Camera, :6-13): origin, yaw = pitch = 0 (looking along +x),
+      fov 90 -- which puts the camera inside the mushroom's bounding box.
+
+    glass_dielectric=True sets material 0's type to DIELECTRIC (the editor's material
+    panel can), so the mushroom and the glass sphere refract (ior 1.5, roughness 0.07)."""
+    scene = generate("default")
+    scene.name = "reference_init_glass" if glass_dielectric else "reference_init"
+    if glass_dielectric:
+        m = scene.materials.copy()
+        m["type"][0] = 1
+        scene.materials = m
+    scene.meshes = [bvh_build(obj_load(obj_path or MUSHROOM_OBJ), bvh)]
+    scene.camera = make_camera(position=(0.0, 0.0, 0.0), yaw=0.0, pitch=0.0, fov=90.0)
+    return scene
+
+
 def generate(name: str, seed: int = 0, via_obj: bool = True, bvh: str = "midpoint") -> HostScene:
     """Synthetic scene -> HostScene. With via_obj the mesh goes through OBJ text and the loader, like
-    LoadModel's parse_obj_file (the atrium is the Sponza-scale OBJ of configs 3-5)."""
+    LoadModel's parse_obj_file (the atrium is the Sponza-scale OBJ of configs 3-5). "reference_init" and
+    "reference_init_glass" are the reference's own Init scene (reference_init)."""
+    if name in REFERENCE_SCENES:
+        return reference_init(glass_dielectric=name.endswith("_glass"), bvh=bvh)
     s = SceneC()
     check(lib.wcpt_scene_generate(name.encode(), seed, C.byref(s)))
     try:
