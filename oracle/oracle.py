@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# bench.py's cpu_baseline points this at its -O3 -march=native build of the same source (WCPT_ORACLE_LIB)
+LIB_PATH = os.environ.get("WCPT_ORACLE_LIB", os.path.join(HERE, "liboracle.so"))
 
 SCENE_DATA_ITEMSIZE = 164
 WORK_FIELDS = ("pixels", "segments", "sphere_tests", "node_pops", "interior_visits", "triangle_tests",

@@ -1,0 +1,114 @@
+"""The C oracle against an independent restatement of the reference (oracle/pt_f64.py: numpy, written from the GLSL
+alone, no code or convention shared with pt_oracle.c, wcpt_libm.h or the kernels).
+
+The kernels are bit-exact with the C oracle, so these tests are what ties both to the GLSL's semantics:
+  * binary32 evaluation of the restatement (numpy per-operation rounding, numpy's float32 libm, true division): most
+    channels bit-identical to the oracle, almost no pixel diverged -- any disagreement left is the libm and the
+    v * RN(1/s) division convention, which shift single ULPs;
+  * binary64 evaluation: pixels within 1e-4 except the few rays whose binary32 decision flips at a threshold (a
+    triangle edge, the Fresnel draw, a grazing sphere) and then diverge chaotically; their share is bounded and of the
+    same order as the divergence a 1-ULP perturbation of the camera causes in the oracle itself;
+  * the exact work counters within 0.5 % in total (binary32: a 1-ULP ray direction can still swap a near/far push
+    or a cull on the atrium's grid-aligned boxes, which changes pops but not the pixel) and within 1 % (binary64,
+    where a flipped decision can change a path's segments without moving its pixel);
+  * attribution: with the oracle's one documented convention (normalize as v * RN(1/|v|)) substituted into the
+    binary32 restatement, >= 99 % of the atrium's channels are bit-identical; what remains is the libm.
+Parity against the reference's execution stays unpinned: this pins the oracle's semantics, not its
+bits."""
+import numpy as np
+import pytest
+
+import oracle
+import pt_f64
+from wcpt import scene
+
+CASES = [  # scene, W, H, maxBounceCount, samples, progressive frames
+    ("cornell", 48, 32, 4, 1, (0, 1)),
+    ("default", 48, 32, 3, 1, (0,)),
+    ("default_dielectric", 48, 32, 3, 1, (0, 1, 7)),
+    ("default_emissive", 48, 32, 3, 2, (0,)),
+    ("atrium", 32, 18, 4, 1, (0,)),
+    ("reference_init", 48, 27, 3, 1, (1, 3)),
+    ("reference_init_glass", 48, 27, 3, 2, (0,)),
+]
+_scenes = {}
+
+
+def _scene(name):
+    if name not in _scenes:
+        _scenes[name] = scene.generate(name)
+    return _scenes[name]
+
+
+def _oracle_rows(s, W, H, b, spp, frames):
+    """The C oracle row by row (counters per row), frames accumulated in order."""
+    img = np.zeros((H, W, 4), np.float32)
+    cnt = {}
+    for y in range(H):
+        acc = None
+        for f in frames:
+            acc, c = oracle.render_scene(s, W, H, max_bounce=b, samples=spp, frame=f, y0=y, rows=1, image=acc)
+        img[y] = acc[0]
+        for k, v in c.items():
+            cnt.setdefault(k, np.zeros(H, np.int64))[y] = v
+    return img, cnt
+
+
+def _restated(s, W, H, b, spp, frames, dtype):
+    img = None
+    for f in frames:
+        img, cnt = pt_f64.render_scene(s, W, H, max_bounce=b, samples=spp, frame=f, image=img, dtype=dtype)
+    return img, cnt
+
+
+@pytest.mark.parametrize("dtype,max_bad,min_exact", [(np.float32, 0.005, 0.85), (np.float64, 0.02, 0.0)],
+                         ids=["binary32", "binary64"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_restatement_agrees_with_oracle(case, dtype, max_bad, min_exact):
+    name, W, H, b, spp, frames = case
+    s = _scene(name)
+    ref, rcnt = _oracle_rows(s, W, H, b, spp, frames)
+    got, gcnt = _restated(s, W, H, b, spp, frames, dtype)
+    diff = np.abs(got[..., :3].astype(np.float64) - ref[..., :3].astype(np.float64)).max(axis=2)
+    bad = ~(diff <= 1e-4)
+    assert bad.mean() <= max_bad, f"{bad.sum()} of {bad.size} pixels diverged"
+    assert diff[~bad].mean() <= 1e-5
+    assert np.mean(got[..., :3].astype(np.float32) == ref[..., :3]) >= min_exact
+    assert np.array_equal(got[..., 3], ref[..., 3])              # alpha = 1.0 (:323)
+    tol = 0.005 if dtype is np.float32 else 0.01
+    for k in rcnt:
+        g, r = (gcnt[k].max(), rcnt[k].max()) if k == "ref_stack_max" else (gcnt[k].sum(), rcnt[k].sum())
+        assert abs(int(g) - int(r)) <= tol * max(1, int(r)), (k, g, r)
+
+
+def test_restatement_rng_matches_kats():
+    """Random.glsl restated (PCG hash, rand overwriting its state) against the SURVEY.md §4 known answers."""
+    assert pt_f64.pcg_hash(np.array([0, 1, 2, 719393, 2073599], np.uint32)).tolist() == [
+        129708002, 2831084092, 2055130248, 1815429807, 2921424543]
+    st = pt_f64.pcg_hash(np.array([0], np.uint32))
+    vals = [float(pt_f64.rand(st)[0]) for _ in range(4)]
+    assert np.allclose(vals, [0.54812092, 0.14715818, 0.19544323, 0.64723909], rtol=0, atol=5e-8)
+    assert int(st[0]) == 2779870596
+
+
+def test_restatement_samples_zero_and_empty_scene():
+    """Edge inputs: samples = 0 divides 0 by 0 (:312, NaN radiance, as the oracle); an empty scene is all sky."""
+    s = _scene("cornell")
+    ref, _ = oracle.render_scene(s, 8, 4, max_bounce=2, samples=0, frame=0)
+    got, _ = pt_f64.render_scene(s, 8, 4, max_bounce=2, samples=0, frame=0)
+    assert np.isnan(ref[..., :3]).all() and np.isnan(got[..., :3]).all()
+
+
+def test_residual_is_the_division_convention_and_libm(monkeypatch):
+    """The binary32 restatement with normalize evaluated as v * RN(1/|v|) (the oracle's and the kernels' documented
+    form) instead of a true division: the atrium frame is then >= 99 % bit-identical to the oracle, so
+    the binary32 disagreement above is that convention plus the libm's last-ULP differences, not a semantic one."""
+    def normalize_rcp(v):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return v * (pt_f64._FT(1.0) / np.sqrt(pt_f64._dot(v, v)))[..., None]
+
+    monkeypatch.setattr(pt_f64, "_normalize", normalize_rcp)
+    s = _scene("atrium")
+    ref, _ = oracle.render_scene(s, 32, 18, max_bounce=4, samples=1, frame=0)
+    got, _ = pt_f64.render_scene(s, 32, 18, max_bounce=4, samples=1, frame=0, dtype=np.float32)
+    assert np.mean(got[..., :3] == ref[..., :3]) >= 0.99

@@ -5,7 +5,10 @@
 // loaded data (a dependent chain, like BVH traversal); with chain=0 the indices come from a PCG stream.
 // coherent=1 makes all 64 lanes of a wave read the same record. Reports lane-loads/s and record-visits/s.
 //
-//   hipcc --offload-arch=gfx950 -O3 -o /tmp/gather_bench tools/gather_bench.hip && /tmp/gather_bench
+//   hipcc --offload-arch=gfx950 -O3 -o tools/gather_bench tools/gather_bench.hip && tools/gather_bench [KiB ...]
+//
+// The last line is a JSON summary: the L2-resident dependent-chain rate (4 MiB table, 4 x 16 B = one 64-B line per
+// visit) is the `peak` of bench.py's memory_latency roofline (profiles/gather_ceiling.json).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -73,7 +76,7 @@ static double run(const uint4* table, uint32_t records, uint32_t steps, uint32_t
     return ms * 1e-3;
 }
 
-int main()
+int main(int argc, char** argv)
 {
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -81,7 +84,13 @@ int main()
     const uint32_t steps = 256;
     uint32_t* out;
     CHECK(hipMalloc(&out, sizeof(uint32_t) * waves * 64u));
-    for (size_t table_bytes : {size_t(64) << 10, size_t(4) << 20, size_t(16) << 20, size_t(512) << 20}) {
+    std::vector<size_t> sizes = {size_t(64) << 10, size_t(4) << 20, size_t(16) << 20, size_t(512) << 20};
+    if (argc > 1) {
+        sizes.clear();
+        for (int i = 1; i < argc; i++) sizes.push_back((size_t)strtoull(argv[i], nullptr, 10) << 10);
+    }
+    std::vector<std::pair<size_t, double>> chain4;
+    for (size_t table_bytes : sizes) {
         const uint32_t records = (uint32_t)(table_bytes / 64);
         uint4* table;
         CHECK(hipMalloc(&table, table_bytes));
@@ -95,6 +104,7 @@ int main()
         rs.push_back({"chain  1x16B", run<1, true, false>(table, records, steps, waves, out), 1});
         rs.push_back({"chain  4x16B", run<4, true, false>(table, records, steps, waves, out), 4});
         rs.push_back({"cohrnt 4x16B", run<4, true, true>(table, records, steps, waves, out), 4});
+        chain4.push_back({table_bytes, (double)waves * 64.0 * steps / rs[3].s * 1e-9});
         for (auto& r : rs) {
             const double visits = (double)waves * 64.0 * steps;
             const double lane_loads = visits * r.loads;
@@ -105,5 +115,12 @@ int main()
         CHECK(hipFree(table));
     }
     CHECK(hipFree(out));
+    printf("{\"chain_64B_glines_per_s\": {");
+    double l2 = 0.0;
+    for (size_t i = 0; i < chain4.size(); i++) {
+        printf("%s\"%zu KiB\": %.2f", i ? ", " : "", chain4[i].first >> 10, chain4[i].second);
+        if (chain4[i].first == (size_t(4) << 20)) l2 = chain4[i].second;
+    }
+    printf("}, \"l2_resident_chain_glines_per_s\": %.2f, \"waves_per_simd\": 8}\n", l2);
     return 0;
 }

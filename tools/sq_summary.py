@@ -24,6 +24,12 @@ def main():
     ap.add_argument("--cycles-per-sec", type=float, default=2.4e9)
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--config", default=None, help="bench config the passes ran (bench.py reads sq_<config>.json)")
+    ap.add_argument("--kernel-id", type=int, default=None, help="wcpt kernel variant (0 megakernel, 2 wavefront)")
+    ap.add_argument("--bound", default=None, choices=["valu_issue", "memory_latency"],
+                    help="the binding resource bench.py's roofline prices against")
+    ap.add_argument("--resource", default=None, help="one-line description of the binding resource")
+    ap.add_argument("--source", default=None, help="where the passes came from (round, script, kernel time)")
     a = ap.parse_args()
     per = defaultdict(list)
     for f in glob.glob(os.path.join(a.dir, "p*", "**", "*counter_collection.csv"), recursive=True):
@@ -42,6 +48,15 @@ def main():
                                     ("active_inst_any", "SQ_ACTIVE_INST_ANY")) if c in m}
     if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
         out["l2_hit_rate"] = round(m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 3)
+    if "SQ_THREAD_CYCLES_VALU" in m and "SQ_ACTIVE_INST_VALU" in m:
+        out["lane_utilisation_valu"] = round(m["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * m["SQ_ACTIVE_INST_VALU"]), 3)
+    out["launches_per_frame"] = a.launches_per_frame
+    for k in ("config", "bound", "resource", "source"):
+        if getattr(a, k) is not None:
+            out[k] = getattr(a, k)
+    if a.kernel_id is not None:
+        out["kernel_name_filter"] = out["kernel"]
+        out["kernel"] = a.kernel_id
     print(json.dumps(out, indent=1))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
