@@ -308,6 +308,9 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          the ranks' streams. Asynchronous, like wcpt_render.
  *   wcpt_group_sync        waits for every rank (and reports a traversal-stack overflow on any of them).
  * Errors leave the group usable; wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains them. */
+/* The row-block split itself, for a host that runs one process per device (then wcpt_set_row_range with the
+ * result): rank r of n renders rows [r*height/n, (r+1)*height/n). Host-only, no device needed. */
+int           wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uint32_t* rows);
 typedef struct wcpt_group wcpt_group;
 int           wcpt_group_create(const int* devices, int n, int root, wcpt_group** out);
 int           wcpt_group_destroy(wcpt_group* g);

@@ -68,3 +68,27 @@ def test_gather_reassembles_frame(tmp_path, world, rgb_only):
     mp.spawn(_worker, args=(world, _free_port(), W, H, out, rgb_only), nprocs=world, join=True)
     full, _ = oracle.render_scene(wscene.generate("cornell"), W, H, max_bounce=4, frame=3)
     assert np.array_equal(np.load(out), full)
+
+
+@pytest.mark.parametrize("height", [1, 7, 8, 135, 1080, 2160, 4099])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 7, 8])
+def test_row_block_bookkeeping_matches_across_hosts(height, n):
+    """The C-ABI split (wcpt_row_block, which wcpt_group_create_screen uses for its ranks) equals the Python host's
+    (wcpt.dist.row_block, which bench.py's ranks use), and the blocks tile the frame exactly: contiguous, disjoint,
+    in rank order, differing by at most one row."""
+    import ctypes as C
+    import wcpt
+    from wcpt.dist import row_block
+    if height < n:
+        pytest.skip("a group needs at least one row per rank")
+    y0, rows = C.c_uint32(), C.c_uint32()
+    nxt, sizes = 0, []
+    for r in range(n):
+        assert wcpt.lib.wcpt_row_block(height, n, r, C.byref(y0), C.byref(rows)) == 0
+        assert (y0.value, rows.value) == row_block(height, n, r)
+        assert y0.value == nxt
+        nxt += rows.value
+        sizes.append(rows.value)
+    assert nxt == height and max(sizes) - min(sizes) <= 1
+    assert wcpt.lib.wcpt_row_block(height, n, n, C.byref(y0), C.byref(rows)) == -1000
+    assert wcpt.lib.wcpt_row_block(height, 0, 0, C.byref(y0), C.byref(rows)) == -1000

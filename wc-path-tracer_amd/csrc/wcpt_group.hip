@@ -176,15 +176,26 @@ wcpt_context* wcpt_group_context(wcpt_group* g, int rank)
     return g->ctx[rank];
 }
 
+int wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uint32_t* rows)
+{
+    if (!y0 || !rows || n == 0 || rank >= n) return WCPT_ERROR_INVALID_ARGUMENT;
+    const uint32_t a = (uint32_t)((uint64_t)rank * height / n);
+    const uint32_t b = (uint32_t)((uint64_t)(rank + 1) * height / n);
+    *y0 = a;
+    *rows = b - a;
+    return WCPT_SUCCESS;
+}
+
 int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
     if (width == 0 || height < (uint32_t)g->n)
         return group_error(WCPT_ERROR_INVALID_ARGUMENT, "%ux%u frame for %d row blocks", width, height, g->n);
     for (int r = 0; r < g->n; r++) {
-        /* the row-block split of SURVEY.md §8(e) (wcpt.dist.row_block): blocks differ by at most one row */
-        const uint32_t y0 = (uint32_t)((uint64_t)r * height / (uint32_t)g->n);
-        const uint32_t y1 = (uint32_t)((uint64_t)(r + 1) * height / (uint32_t)g->n);
+        /* the row-block split of SURVEY.md §8(e) (wcpt_row_block): blocks differ by at most one row */
+        uint32_t y0 = 0, rows = 0;
+        (void)wcpt_row_block(height, (uint32_t)g->n, (uint32_t)r, &y0, &rows);
+        const uint32_t y1 = y0 + rows;
         /* a resized frame first keeps the previous block (clipped to the new height), so no rank ever allocates the
          * whole frame; a fresh context takes its block before its first screen */
         int rc = g->width ? wcpt_create_screen(g->ctx[r], width, height) : WCPT_SUCCESS;

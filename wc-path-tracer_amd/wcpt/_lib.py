@@ -159,6 +159,7 @@ _PROTOTYPES = {
     "wcpt_string_free": (None, [C.c_void_p]),
     "wcpt_selftest_device": (_i, [_p, _i, _p, _p, _p, _u32]),
     "wcpt_runtime_version": (_i, [C.POINTER(_i)]),
+    "wcpt_row_block": (_i, [_u32, _u32, _u32, C.POINTER(_u32), C.POINTER(_u32)]),
     "wcpt_group_create": (_i, [C.POINTER(_i), _i, _i, C.POINTER(_p)]),
     "wcpt_group_destroy": (_i, [_p]),
     "wcpt_group_context": (_p, [_p, _i]),
