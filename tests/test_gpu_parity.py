@@ -993,3 +993,18 @@ def test_reference_init_full_size_rows(gpu_ctx, kernel, name):
         assert_close(img[y0:y0 + 8], ref)
     _, rcnt = oracle.render_scene(s, W, H, max_bounce=3, frame=3, threads=16)
     assert cnt == rcnt
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_deeper_than_reference_stack_counted(gpu_ctx, kernel):
+    """A BVH chain 40 levels deep (tests/deep_tree.py) that drives the reference's stack past its 32 entries
+    (pathTracer.comp:151, undefined behaviour there): this implementation renders it with its 48-entry stack,
+    bit-exact against the oracle, and the counting kernel reports the same overflowing segments and deepest stack."""
+    from deep_tree import deep_chain_scene
+    s = deep_chain_scene(get_scene("default"), levels=40)
+    W, H = 48, 32
+    img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=2, kernel=kernel)
+    ref, rcnt = oracle.render_scene(s, W, H, max_bounce=2, threads=8)
+    assert_close(img, ref)
+    assert cnt == rcnt
+    assert rcnt["ref_stack_max"] == 41 and rcnt["ref_stack_overflow_segments"] > 0

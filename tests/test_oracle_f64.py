@@ -112,3 +112,16 @@ def test_residual_is_the_division_convention_and_libm(monkeypatch):
     ref, _ = oracle.render_scene(s, 32, 18, max_bounce=4, samples=1, frame=0)
     got, _ = pt_f64.render_scene(s, 32, 18, max_bounce=4, samples=1, frame=0, dtype=np.float32)
     assert np.mean(got[..., :3] == ref[..., :3]) >= 0.99
+
+
+def test_reference_stack_overflow_counted_alike():
+    """A BVH chain 40 levels deep (tests/deep_tree.py): both restatements count the same segments writing past the
+    reference's nodeStack[32] and the same deepest stack (levels + 1 entries)."""
+    from deep_tree import deep_chain_scene
+    s = deep_chain_scene(_scene("default"), levels=40)
+    assert s.meshes[0].depth() == 41
+    _, rc = oracle.render_scene(s, 24, 16, max_bounce=2, frame=0)
+    _, gc = pt_f64.render_scene(s, 24, 16, max_bounce=2, frame=0, dtype=np.float32)
+    assert rc["ref_stack_max"] == int(gc["ref_stack_max"].max()) == 41
+    assert rc["ref_stack_overflow_segments"] > 0
+    assert rc["ref_stack_overflow_segments"] == int(gc["ref_stack_overflow_segments"].sum())
