@@ -115,6 +115,12 @@ def roofline(args, tot, render_s, frame_s) -> dict:
                 "unit": "G VALU issue-cycles/s", "frac": round(achieved / VALU_PEAK_GCYCLES, 3),
                 "source": f"SQ_INSTS_VALU {valu:.4g}/render ({sq.get('source', 'profiles')}) x {CYCLES_PER_VALU} "
                           f"cycles over the live render time; peak {SIMDS} SIMDs x {CLOCK_GHZ} GHz"}
+        ceil = _json_field("valu_ceiling.json", "issue_gcycles_per_s")
+        if ceil:
+            # the best VALU rate measured on the chip (independent FMA chains, 8 waves/SIMD): the clock under load
+            # sits below the 2.4 GHz spec, so this is the attainable ceiling
+            head["measured_ceiling"] = ceil
+            head["measured_frac"] = round(achieved / ceil, 3)
     elif bound == "memory_latency":
         ceil = _gather_ceiling()
         lines = (tot["interior_visits"] + tot["triangle_tests"]) / steps
@@ -133,12 +139,16 @@ def roofline(args, tot, render_s, frame_s) -> dict:
     return head
 
 
-def _gather_ceiling() -> float:
-    p = os.path.join(ROOT, "profiles", "gather_ceiling.json")
+def _json_field(name: str, key: str):
     try:
-        return float(json.load(open(p))["l2_resident_chain_glines_per_s"])
-    except (OSError, ValueError, KeyError):
-        return 230.0  # DESIGN.md §3 table (4 MiB, L2-resident), round 1
+        return float(json.load(open(os.path.join(ROOT, "profiles", name)))[key])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def _gather_ceiling() -> float:
+    v = _json_field("gather_ceiling.json", "l2_resident_chain_glines_per_s")
+    return v if v else 207.4  # profiles/r03_gather_ceiling.log (4 MiB, L2-resident)
 
 
 def _cpu_model() -> str:
