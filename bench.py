@@ -251,6 +251,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", type=int, default=-1,
                     help="0 megakernel, 2 wavefront, -1 per-config default (DEFAULT_KERNEL)")
+    ap.add_argument("--wf-pipes", type=int, default=0,
+                    help="wavefront kernel: concurrent pipelines (WCPT_OPTION_WF_PIPES; 0 = the library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--pmc-json", default=None,
@@ -294,6 +296,8 @@ def main():
         device = local % max(1, wcpt.device_count())
         ctx = wcpt.Context(device)
         ctx.set_kernel(args.kernel)
+        if args.wf_pipes:
+            ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
         dev = wcpt.DeviceScene(ctx, scene)
         ctx.create_screen(W, H)
         addrs = dev.addresses()
@@ -323,6 +327,8 @@ def main():
         ctx = wcpt.Context(device)
         ctx.set_stream(stream.cuda_stream)
         ctx.set_kernel(args.kernel)
+        if args.wf_pipes:
+            ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
         dev = wcpt.DeviceScene(ctx, scene)
         ctx.create_screen(W, H)
         ctx.set_row_range(y0, rows)

@@ -84,8 +84,11 @@ extern "C" {
  * 20). */
 #define WCPT_OPTION_WF_REFILL 8
 /* Megakernel tile order: 0 each XCD walks a contiguous band of 8x8 tiles; 1 scattered (tile b * m mod tiles), so the
- * tiles resident on a CU at once come from all over the frame; 2 (default) scattered when the launch fits in about
- * one round of resident waves (small row blocks: the tail is the most loaded CU), banded otherwise. Same results. */
+ * tiles resident on a CU at once come from all over the frame; 3, 4, 5, 6 XCD bands striped by 1, 2, 4, 8 tile rows
+ * (XCD x walks the stripes s = x mod 8, so every XCD sees every part of the frame while neighbouring tiles stay
+ * together); 2 (default) scattered when the launch fits in about one round of resident waves (small row blocks: the
+ * tail is the most loaded CU), stripes of one tile row otherwise (a scene whose cost is concentrated in one region of
+ * the image no longer leaves one XCD with it). Same results. */
 #define WCPT_OPTION_MK_TILE_ORDER 9
 /* Wavefront: concurrent pipelines (1..4, default 2). Pipeline j renders the 8x8 tiles t with t % K == j on its own
  * stream, so one pipeline's trace tail (a few slow rays) overlaps another's bulk. Same results. */

@@ -776,12 +776,15 @@ def test_random_scenes_match_oracle(gpu_ctx, seed, kernel):
     assert cnt == rcnt
 
 
+@pytest.mark.parametrize("order", [0, 1, 3, 5])
 @pytest.mark.parametrize("name,W,H,bounces,spp,rows", [
-    ("cornell", 67, 45, 4, 3, None), ("atrium", 96, 54, 4, 1, None), ("cornell", 1920, 1080, 4, 1, 135)])
-def test_scattered_tile_order_matches_oracle(gpu_ctx, name, W, H, bounces, spp, rows):
-    """WCPT_OPTION_MK_TILE_ORDER = 1 (scattered tiles) changes only which wave renders which tile."""
+    ("cornell", 67, 45, 4, 3, None), ("atrium", 96, 54, 4, 1, None), ("cornell", 1920, 1080, 4, 1, 135),
+    ("reference_init", 64, 72, 3, 2, None)])   # 8 x 9 tiles: a multiple of 8, tile rows not
+def test_tile_orders_match_oracle(gpu_ctx, order, name, W, H, bounces, spp, rows):
+    """WCPT_OPTION_MK_TILE_ORDER 0 (XCD bands), 1 (scattered), 3 and 5 (XCD bands striped by 1 and 4 tile rows) change only which
+    wave renders which tile: every tile exactly once, same image and counters as the oracle."""
     s = get_scene(name)
-    gpu_ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, 1)
+    gpu_ctx.set_option(wcpt._lib.OPTION_MK_TILE_ORDER, order)
     try:
         img, cnt = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=1, rows=rows,
                               init=np.zeros((rows or H, W, 4), np.float32))

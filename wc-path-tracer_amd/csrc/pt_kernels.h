@@ -28,7 +28,7 @@ struct LaunchArgs {
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
-    uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto (WCPT_OPTION_MK_TILE_ORDER) */
+    uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto, 3-6 striped bands (WCPT_OPTION_MK_TILE_ORDER) */
     float4* image;
     float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
     uint32_t wire_ch;            /* its channels per pixel: 3 or 4 */

@@ -31,10 +31,31 @@ __device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTot
 {
     const uint32_t b = blockIdx.x;
     uint32_t t = b;
-    if (scatter != 0u)
-        t = (uint32_t)(((uint64_t)b * scatter) % tilesTotal);
-    else if ((tilesTotal & 7u) == 0u)
+    if (scatter & 1u) {
+        t = (uint32_t)(((uint64_t)b * scatter) % tilesTotal);   /* odd: scattered, multiplier `scatter` */
+    } else if ((tilesTotal & 7u) == 0u) {
+        /* blocks go to the XCDs round-robin (block b -> XCD b mod 8): XCD x walks the x-th eighth of a tile list */
         t = (b & 7u) * (tilesTotal >> 3) + (b >> 3);
+        if (scatter != 0u) {
+            /* even scatter = 2h: striped list. Stripes of h tile rows, listed by (stripe mod 8, stripe / 8), each in
+             * raster order, so XCD x walks (about) the stripes s = x mod 8: neighbouring tiles stay together on an
+             * XCD, and every XCD sees every part of the frame (one contiguous band per XCD can leave a few XCDs with
+             * the heavy regions of the image) */
+            const uint32_t h = scatter >> 1;
+            const uint32_t tilesY = tilesTotal / tilesX;
+            const uint32_t full = tilesY / (8u * h), rem = tilesY % (8u * h);
+            for (uint32_t j = 0; j < 8u; j++) {
+                const uint32_t part = rem > j * h ? min(rem - j * h, h) : 0u;
+                const uint32_t seg = (full * h + part) * tilesX;   /* tiles of the rows in stripes s = j mod 8 */
+                if (t < seg) {
+                    const uint32_t lr = t / tilesX;
+                    t = (((lr / h) * 8u + j) * h + lr % h) * tilesX + t % tilesX;
+                    break;
+                }
+                t -= seg;
+            }
+        }
+    }
     tx = t % tilesX;
     ty = t / tilesX;
 }
@@ -346,7 +367,12 @@ static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stre
 {
     /* scattered tile order: block b renders tile (b * m) mod tiles for an m coprime with tiles near 0.618 * tiles,
      * so the tiles resident on one CU at once come from all over the frame */
-    uint32_t scatter = 0;
+    /* 3, 4, 5, 6: striped XCD bands of 1, 2, 4, 8 tile rows (tile_of_block: even scatter = 2 x stripe height);
+     * 2 (auto, default): scattered for a launch of about one round of resident waves (below), else stripes of one tile
+     * row. Measured (round 3, 10 frames x 4 interleaved rounds): the reference's Init scene 1.91 ms (bands) -> 1.48 ms
+     * (stripes of 1; 2 / 4 / 8 rows: 1.50 / 1.69 / 1.98 ms; scattered 1.52), the atrium on the megakernel 12.15 ->
+     * 11.24 ms; the Cornell box 0.379 -> 0.382 ms (its tiles cost alike, so bands only keep neighbours together) */
+    uint32_t scatter = a.mk_tile_order >= 3 ? (2u << (a.mk_tile_order - 3)) : (a.mk_tile_order == 2 ? 2u : 0u);
     const bool one_round = (uint64_t)tiles <= 16ull * (uint64_t)mk.cus; /* <= ~4 resident waves per SIMD */
     if ((a.mk_tile_order == 1 || (a.mk_tile_order == 2 && one_round)) && tiles > 2) {
         uint32_t m = (uint32_t)((uint64_t)tiles * 618034u / 1000000u) | 1u;

@@ -624,7 +624,7 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         ctx->wf_pipes = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_MK_TILE_ORDER:
-        if (value < 0 || value > 2) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "tile order %d", value);
+        if (value < 0 || value > 6) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "tile order %d", value);
         ctx->mk_tile_order = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PACKED_REFS:
