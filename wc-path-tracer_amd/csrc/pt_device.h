@@ -313,6 +313,24 @@ __device__ __forceinline__ NodeV load_node(gnode_ptr bvh, uint32_t i)
     n.b = reinterpret_cast<const WCPT_GLOBAL v4u*>(p)[1];
     return n;
 }
+/* The child pair (left, left + 1) of an interior node through a buffer resource over the BVH (draws whose BVH is a
+ * known context buffer of < 2^24 nodes: table word 2's high half holds the node count): the four loads take one VGPR
+ * byte offset (buffer_load_dwordx4 v_off, s[rsrc] offen offset:0/16/32/48) instead of two 64-bit lane addresses
+ * (v_lshlrev_b64 + v_lshl_add_u64 each), and an index past the buffer reads a zero node instead of other memory.
+ * Same bytes for every node in the buffer. */
+constexpr int kBufferDword3 = 0x00020000; /* gfx9 raw buffer resource word 3 (composable_kernel's value for gfx9) */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(gnode_ptr bvh, uint32_t nodes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc((void*)bvh, (short)0, (int)(nodes * 32u), kBufferDword3);
+}
+__device__ __forceinline__ void load_pair_rsrc(__amdgpu_buffer_rsrc_t r, uint32_t left, NodeV& L, NodeV& R)
+{
+    const int off = (int)(left << 5);
+    L.a = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    L.b = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
+    R.a = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, off + 32, 0, 0));
+    R.b = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off + 48, 0, 0));
+}
 /* (leftNodeOrTriangleIndex, triangleCount) of node i: bytes 24..31 */
 __device__ __forceinline__ uint2 load_node_lc(gnode_ptr bvh, uint32_t i)
 {
@@ -682,9 +700,25 @@ __device__ __forceinline__ uint32_t leaf_record(uint32_t first, uint32_t count, 
  * lim3 - first is a multiple of 3, and count <= M holds for a multiple M of 3 exactly when 3 * ceil(count / 3) <= M.
  * It is written as first <= lim3 && count <= lim3 - first, which cannot wrap; lim3 < 2^24 for these draws, so an
  * accepted first is < 2^24 and the 24-bit alignment test above is exact for it. */
+/* v_mul_u32_u24 (full rate). __umul24 is not enough here: only the low 24 bits of its product are used, so the
+ * optimizer drops its 24-bit operand masks and the backend then emits the quarter-rate v_mul_lo_u32 (seen in the ISA
+ * of both kernels). */
+#ifndef WCPT_MUL24_ASM
+#define WCPT_MUL24_ASM 1
+#endif
+__device__ __forceinline__ uint32_t mul_u32_u24(uint32_t a, uint32_t b_uniform)
+{
+#if WCPT_MUL24_ASM
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(b_uniform), "v"(a));
+    return r;
+#else
+    return __umul24(a, b_uniform);
+#endif
+}
 __device__ __forceinline__ uint32_t leaf_record_off24(uint32_t first, uint32_t count, uint32_t lim3)
 {
-    const bool aligned = (__umul24(first, 0xAAAAABu) & 0xFFFFFFu) <= 0x555555u;
+    const bool aligned = (mul_u32_u24(first, 0xAAAAABu) & 0xFFFFFFu) <= 0x555555u;
     return (aligned && first <= lim3 && count <= lim3 - first) ? first * 16u : kNoRecord;
 }
 /* leaf_record as a byte offset for any draw (records beyond 4 GiB take the index path) */

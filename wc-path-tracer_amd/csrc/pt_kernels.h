@@ -93,6 +93,7 @@ struct WfPipes {
     hipStream_t aux[kWfMaxPipes] = {};   /* [1..K-1]: created on first use, on the context's device */
     hipEvent_t fork = nullptr;
     hipEvent_t join[kWfMaxPipes] = {};
+    hipEvent_t ready[kWfMaxPipes] = {};  /* pipeline j's init has run (WCPT_WF_START_TOGETHER) */
 };
 
 /* Megakernel launch state, per context. */

@@ -170,6 +170,9 @@ enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 
 #ifndef WCPT_WF_REC_OFF24
 #define WCPT_WF_REC_OFF24 1
 #endif
+#ifndef WCPT_WF_PAIR_RSRC
+#define WCPT_WF_PAIR_RSRC 1
+#endif
 struct Geom {
     gtri_ptr tris;
     uint32_t ntri;
@@ -179,6 +182,8 @@ struct Geom {
     gnode_ptr bvh;
     gu32_ptr indices;
     gf32_ptr vertices;
+    uint32_t nodes;                /* BVH node count when the BVH is a known context buffer of < 2^24 nodes, else 0 */
+    __amdgpu_buffer_rsrc_t rsrc;   /* buffer resource over those nodes (load_pair_rsrc) */
 };
 
 __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ draws,
@@ -193,6 +198,8 @@ __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ 
     g.bvh = as_nodes(draws[d].bvhBuffer);
     g.indices = as_u32(draws[d].indexBuffer);
     g.vertices = as_f32(draws[d].vertexBuffer);
+    g.nodes = g.packed ? (uint32_t)(tri_records[kTriTableWords * d + 2u] >> 32) : 0u;
+    g.rsrc = node_rsrc(g.bvh, g.nodes);
     return g;
 }
 
@@ -239,7 +246,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     stk.sp = 0;
     Counters cnt = {};
     bool overflow = false;
-    Geom g0 = {nullptr, 0u, 0u, false, false, nullptr, nullptr, nullptr}, gl = g0;
+    Geom g0 = {}, gl = g0;
     if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
 
     bool has = false, drained = false;
@@ -362,8 +369,13 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
             }
             diag_mark<DIAG>(tim, tprev, 3); /* pop */
             if (has && mode == kModeInterior) {
-                const NodeV L = load_node(g.bvh, ca);
-                const NodeV R = load_node(g.bvh, ca + 1);
+                NodeV L, R;
+                if (WCPT_WF_PAIR_RSRC && g.nodes) {
+                    load_pair_rsrc(g.rsrc, ca, L, R);
+                } else {
+                    L = load_node(g.bvh, ca);
+                    R = load_node(g.bvh, ca + 1);
+                }
                 float l0, l1, r0, r1;
                 node_box(ray, L, l0, l1);
                 node_box(ray, R, r0, r1);
@@ -618,6 +630,7 @@ void wf_release(WfPipes& w)
         wf_release(w.pipe[j]);
         if (w.aux[j]) (void)hipStreamDestroy(w.aux[j]);
         if (w.join[j]) (void)hipEventDestroy(w.join[j]);
+        if (w.ready[j]) (void)hipEventDestroy(w.ready[j]);
     }
     if (w.fork) (void)hipEventDestroy(w.fork);
     if (w.result) (void)hipFree(w.result);
@@ -720,10 +733,10 @@ static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b
                                               s.sort_order, (int)P, 0, 32, stream);
 }
 
-/* One pipeline: init + samples*(maxBounce+1) trace/shade iterations over the tiles t with t % npipes == pipe. */
-static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, float4* result,
-                              uint32_t pipe, uint32_t npipes, bool sort_rays, int ldsn, int cus, uint32_t trace_grid,
-                              uint32_t shade_grid, hipStream_t stream)
+/* One pipeline: init (pipe_begin) + samples*(maxBounce+1) trace/shade iterations (pipe_iterate) over the tiles t with
+ * t % npipes == pipe. */
+static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, float4* result,
+                             uint32_t pipe, uint32_t npipes, int cus, hipStream_t stream, WfBuffers& b)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
@@ -734,10 +747,8 @@ static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const W
     hipError_t e = wf_reserve(s, P);
     if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
-    const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
     e = hipMemsetAsync(s.ctr, 0, 4 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    WfBuffers b;
     b.in = s.soa[0];
     b.out = s.soa[1];
     b.result = result;
@@ -760,8 +771,19 @@ static hipError_t launch_pipe(const LaunchArgs& a, int mode, WfState& s, const W
     else
         hipLaunchKernelGGL(dev::wf_init<false>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
                            a.W, a.H, a.y0, a.rows, tilesX, total, pipe, npipes, a.counters);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32_t pipe, uint32_t npipes,
+                               bool sort_rays, int ldsn, int cus, uint32_t trace_grid, uint32_t shade_grid,
+                               hipStream_t stream, WfBuffers b)
+{
+    const uint32_t tilesX = (a.W + 7u) / 8u;
+    const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
+    if (pipe >= tiles) return hipSuccess;
+    const uint32_t P = min(((tiles - pipe + npipes - 1u) / npipes) * 64u, a.W * a.rows); /* as pipe_begin */
+    const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
+    hipError_t e = hipSuccess;
     /* each iteration advances every live path by one segment; a path needs <= samples*(maxBounce+1) */
     uint64_t iters = (uint64_t)a.sd.samples * ((uint64_t)a.sd.maxBounceCount + 1ull);
     if (iters > (1ull << 20)) iters = 1ull << 20; /* bounded; WCPT documents the cap */
@@ -826,7 +848,12 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
 #endif
     e = wf_reserve_result(w, (uint64_t)a.W * a.rows);
     if (e != hipSuccess) return e;
-    if (K == 1) return launch_pipe(a, mode, s0, s0, w.result, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream);
+    WfBuffers bs[kWfMaxPipes];
+    if (K == 1) {
+        e = pipe_begin(a, mode, s0, s0, w.result, 0, 1, cus, stream, bs[0]);
+        if (e != hipSuccess) return e;
+        return pipe_iterate(a, mode, s0, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream, bs[0]);
+    }
 
     /* fork: pipelines 1..K-1 run on their own streams after everything already queued on the context's stream */
     if (!w.fork) {
@@ -851,8 +878,24 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     }
     hipError_t first = hipSuccess;
     for (uint32_t j = 0; j < K && first == hipSuccess; j++)
-        first = launch_pipe(a, mode, w.pipe[j], s0, w.result, j, K, false, ldsn, cus, trace_grid, shade_grid,
-                            j == 0 ? stream : w.aux[j]);
+        first = pipe_begin(a, mode, w.pipe[j], s0, w.result, j, K, cus, j == 0 ? stream : w.aux[j], bs[j]);
+#ifndef WCPT_WF_START_TOGETHER
+#define WCPT_WF_START_TOGETHER 0
+#endif
+    if (WCPT_WF_START_TOGETHER && first == hipSuccess) {
+        /* every pipeline's first trace waits for all the inits: the persistent trace grids then start on an idle
+         * chip together instead of the first one being placed around the other pipelines' init blocks */
+        for (uint32_t j = 0; j < K && first == hipSuccess; j++) {
+            if (!w.ready[j]) first = hipEventCreateWithFlags(&w.ready[j], hipEventDisableTiming);
+            if (first == hipSuccess) first = hipEventRecord(w.ready[j], j == 0 ? stream : w.aux[j]);
+        }
+        for (uint32_t j = 0; j < K && first == hipSuccess; j++)
+            for (uint32_t i = 0; i < K && first == hipSuccess; i++)
+                if (i != j) first = hipStreamWaitEvent(j == 0 ? stream : w.aux[j], w.ready[i], 0);
+    }
+    for (uint32_t j = 0; j < K && first == hipSuccess; j++)
+        first = pipe_iterate(a, mode, w.pipe[j], j, K, false, ldsn, cus, trace_grid, shade_grid,
+                             j == 0 ? stream : w.aux[j], bs[j]);
     /* join: the context's stream continues after every pipeline (also after a failed enqueue) */
     for (uint32_t j = 1; j < K; j++) {
         e = hipEventRecord(w.join[j], w.aux[j]);

@@ -328,7 +328,10 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
         if (dc[d].indexCount < (1u << 24)) flags |= 2u; /* pt_device.h kTriFlagIndex24 */
         flags |= (uint64_t)nvert << 32;                 /* pt_device.h draw_vertex_count: bounds the index path */
-        const uint64_t entry[W] = {addr, addr + t.pair_offset, ntri, flags, ctx->tri_table[W * d + 4]};
+        /* word 2: ntri, and in its high half the BVH node count when packed refs apply (the buffer-resource node loads
+         * of pt_device.h load_pair_rsrc cover exactly those nodes) */
+        const uint64_t word2 = (uint64_t)ntri | ((flags & 1u) ? (nodes << 32) : 0ull);
+        const uint64_t entry[W] = {addr, addr + t.pair_offset, word2, flags, ctx->tri_table[W * d + 4]};
         for (uint64_t w = 0; w < W; w++) {
             if (ctx->tri_table[W * d + w] != entry[w]) {
                 ctx->tri_table[W * d + w] = entry[w];
