@@ -45,6 +45,7 @@ def main():
         out["trace_phase_share"] = {k: round(v / tot, 4) for k, v in
                                     zip(("fetch", "leaf", "interior", "pop", "epilogue"), t[:5])}
         out["trace_waves"], out["trace_iterations"] = t[5], t[6]
+        out["trace_tail_share"] = round(t[7] / tot, 4)   # wave-time after the wave found the queue empty
         if t[6]:
             out["trace_cycles_per_iteration"] = round(tot / t[6], 1)
             out["trace_iterations_per_wave"] = round(t[6] / max(1, t[5]), 1)

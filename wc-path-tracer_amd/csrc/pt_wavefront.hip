@@ -204,7 +204,8 @@ __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ 
 }
 
 /* DIAG builds only: per-wave cycle timers (s_memtime) of the trace loop's phases, summed over waves into
- * b.diag[0..4] = {fetch+loop, leaf, interior, pop, epilogue}, [5] = waves, [6] = loop iterations. The stamps
+ * b.diag[0..4] = {fetch+loop, leaf, interior, pop, epilogue}, [5] = waves, [6] = loop iterations, [7] = the waves'
+ * time after they found the queue empty (the launch's tail). The stamps
  * add their own cost; read the shares, not the totals (cdna_hip_programming.md §7, In-kernel stamps). */
 constexpr int kDiagTimers = 8;
 template <bool DIAG>
@@ -268,6 +269,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     Ray ray;
     uint64_t tim[kDiagTimers] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tprev = DIAG ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t t_drain = 0; /* DIAG: when this wave found the queue empty (its tail starts) */
 
     /* Start draw command d, or the next one whose root survives the cull (:152-162); kModeDone past the last. */
     auto start_draw = [&]() {
@@ -341,6 +343,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 need &= ~__ballot(take);
             }
         }
+        if (DIAG && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memtime();
         if (!__ballot(has)) break;
         diag_mark<DIAG>(tim, tprev, 0);
         {
@@ -445,6 +448,7 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     flush_counters<COUNT>(cnt, counters);
     if (DIAG && lane == 0) {
         tim[5] += 1; /* waves */
+        if (t_drain) tim[7] += __builtin_amdgcn_s_memtime() - t_drain; /* tail: queue empty, lanes finishing */
         for (int k = 0; k < kDiagTimers; k++) atomicAdd(&b.diag[k], (unsigned long long)tim[k]);
     }
 }
