@@ -168,8 +168,12 @@ def _native_oracle() -> tuple[str, str]:
     build if no C compiler is available."""
     import subprocess
     import tempfile
+    import atexit
+    import shutil
     flags = "-O3 -march=native -ffp-contract=off -fno-math-errno -fPIC -std=c11 -shared -pthread"
-    out = os.path.join(tempfile.mkdtemp(prefix="wcpt_baseline_"), "liboracle_native.so")
+    tmp = tempfile.mkdtemp(prefix="wcpt_baseline_")
+    atexit.register(shutil.rmtree, tmp, True)  # the loaded library stays mapped after its file is removed
+    out = os.path.join(tmp, "liboracle_native.so")
     src = os.path.join(ROOT, "oracle", "pt_oracle.c")
     try:
         subprocess.run(["gcc", *flags.split(), "-o", out, src, "-lm"], check=True, capture_output=True, timeout=120)

@@ -86,9 +86,10 @@ extern "C" {
 /* Megakernel tile order: 0 each XCD walks a contiguous band of 8x8 tiles; 1 scattered (tile b * m mod tiles), so the
  * tiles resident on a CU at once come from all over the frame; 3, 4, 5, 6 XCD bands striped by 1, 2, 4, 8 tile rows
  * (XCD x walks the stripes s = x mod 8, so every XCD sees every part of the frame while neighbouring tiles stay
- * together); 2 (default) scattered when the launch fits in about one round of resident waves (small row blocks: the
- * tail is the most loaded CU), stripes of one tile row otherwise (a scene whose cost is concentrated in one region of
- * the image no longer leaves one XCD with it). Same results. */
+ * together); 2 (default) cost-ordered: every render records each tile's time, and after the first render of a frame
+ * geometry (width, rows, first row) and every 64 renders the tiles are sorted by it, longest first, for the renders
+ * that follow (the launch's last round then holds the short tiles). Until the first sort: scattered when the launch
+ * fits in about one round of resident waves, stripes of one tile row otherwise. Same results in every order. */
 #define WCPT_OPTION_MK_TILE_ORDER 9
 /* Wavefront: concurrent pipelines (1..4, default 2). Pipeline j renders the 8x8 tiles t with t % K == j on its own
  * stream, so one pipeline's trace tail (a few slow rays) overlaps another's bulk. Same results. */

@@ -1011,3 +1011,42 @@ def test_deeper_than_reference_stack_counted(gpu_ctx, kernel):
     assert_close(img, ref)
     assert cnt == rcnt
     assert rcnt["ref_stack_max"] == 41 and rcnt["ref_stack_overflow_segments"] > 0
+
+
+@pytest.mark.parametrize("name,W,H,bounces,spp", [("cornell", 67, 45, 4, 2), ("reference_init", 96, 64, 3, 1)])
+def test_cost_ordered_tiles_match_oracle(name, W, H, bounces, spp):
+    """The default tile order becomes longest-first after the first render of a geometry (the renders record each
+    tile's time; pt_kernels.hip cost_order_sort). Progressive frames through that order, then a row range and a resize
+    (new geometries: back to the built-in order, then sorted again), all bit-exact against the oracle."""
+    s = get_scene(name)
+    with wcpt.Context(0) as ctx:
+        dev = wcpt.DeviceScene(ctx, s)
+        try:
+            ctx.create_screen(W, H)
+            acc = None
+            for f in range(5):
+                sd = s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f)
+                ctx.render(sd, *dev.addresses())
+                acc, _ = oracle.render_scene(s, W, H, sd=sd, image=acc, threads=8)
+            ctx.sync()
+            assert_close(ctx.readback(H), acc)
+            ctx.set_row_range(8, 24)                  # a row block: another geometry
+            blk = None
+            for f in range(3):
+                sd = s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f)
+                ctx.render(sd, *dev.addresses())
+                blk, _ = oracle.render_scene(s, W, H, sd=sd, y0=8, rows=24, image=blk, threads=8)
+            ctx.sync()
+            assert_close(ctx.readback(24), blk)
+            ctx.set_row_range(0, 0)
+            W2, H2 = W + 16, H - 9
+            ctx.resize(W2, H2)
+            acc = None
+            for f in range(3):
+                sd = s.scene_data(W2, H2, max_bounce=bounces, samples=spp, frame=f)
+                ctx.render(sd, *dev.addresses())
+                acc, _ = oracle.render_scene(s, W2, H2, sd=sd, image=acc, threads=8)
+            ctx.sync()
+            assert_close(ctx.readback(H2), acc)
+        finally:
+            dev.free()

@@ -99,7 +99,22 @@ struct WfPipes {
 /* Megakernel launch state, per context. */
 struct MkState {
     int cus = 0;               /* CU count of the context's device (0 = not yet queried) */
+    /* Cost-ordered tiles (WCPT_OPTION_MK_TILE_ORDER 2): every render records each tile's time; after the first render
+     * of a frame geometry and then every kResortEvery renders the tiles are sorted by it, longest first, and the
+     * following renders take that order (pt_kernels.hip launch_megakernel). */
+    void* mem = nullptr;       /* cost | sorted keys | iota | order, `cap` u32 each, then the sort's scratch */
+    uint32_t cap = 0;
+    uint32_t* cost = nullptr;
+    uint32_t* keys = nullptr;
+    uint32_t* iota = nullptr;
+    uint32_t* order = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    uint32_t geom_w = 0, geom_rows = 0, geom_y0 = 0, geom_tiles = 0; /* geometry the costs and order belong to */
+    uint32_t renders = 0;      /* renders of that geometry */
+    bool order_valid = false;
 };
+void mk_release(MkState& mk);
 
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD
  * diagnostics (ballot-based step counters, tools/diag.py). */

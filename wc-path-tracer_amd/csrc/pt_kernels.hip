@@ -10,6 +10,7 @@
  * __ballot inside the traversal loop (tools/diag.py only — kept out of the COUNT build the parity tests use).
  */
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "pt_device.h"
 #include "pt_kernels.h"
@@ -26,12 +27,14 @@ constexpr uint32_t kTileW = WCPT_TILE_W, kTileH = 64u / WCPT_TILE_W;
 /* Pixel tile -> block mapping. Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
  * "Workgroup dispatch"); remapping the linear block id so that each XCD walks a contiguous band of tiles
  * keeps neighbouring (coherent) tiles on one XCD's L2. Speed only; any placement is correct. */
-__device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTotal, uint32_t scatter, uint32_t& tx,
-                                              uint32_t& ty)
+__device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTotal, uint32_t scatter,
+                                              const uint32_t* __restrict__ order, uint32_t& tx, uint32_t& ty)
 {
     const uint32_t b = blockIdx.x;
     uint32_t t = b;
-    if (scatter & 1u) {
+    if (order != nullptr) {
+        t = order[b]; /* cost-ordered: a permutation of [0, tilesTotal), longest tile first */
+    } else if (scatter & 1u) {
         t = (uint32_t)(((uint64_t)b * scatter) % tilesTotal);   /* odd: scattered, multiplier `scatter` */
     } else if ((tilesTotal & 7u) == 0u) {
         /* blocks go to the XCDs round-robin (block b -> XCD b mod 8): XCD x walks the x-th eighth of a tile list */
@@ -121,11 +124,13 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
                                                     float4* __restrict__ image, float* __restrict__ wire,
                                                     uint32_t wire_ch, uint32_t W, uint32_t H, uint32_t y0,
                                                     uint32_t rows, uint32_t tilesX, uint32_t tilesTotal,
-                                                    uint32_t scatter, uint32_t* __restrict__ status,
+                                                    uint32_t scatter, const uint32_t* __restrict__ tile_order,
+                                                    uint32_t* __restrict__ tile_cost, uint32_t* __restrict__ status,
                                                     unsigned long long* __restrict__ counters)
 {
+    const uint64_t c0 = (!COUNT && tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
     uint32_t tx, ty;
-    tile_of_block(tilesX, tilesTotal, scatter, tx, ty);
+    tile_of_block(tilesX, tilesTotal, scatter, tile_order, tx, ty);
     const uint32_t lx = tx * kTileW + (threadIdx.x % kTileW);
     const uint32_t ly = ty * kTileH + (threadIdx.x / kTileW);
     Counters cnt = {};
@@ -150,6 +155,13 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
     }
     if (overflow) atomicOr(status, 1u);
     flush_counters<COUNT>(cnt, counters);
+    if (!COUNT && tile_cost && (threadIdx.x & 63u) == 0u) {
+        /* this tile's time, for the next renders' order: a running average (each frame draws new bounce directions,
+         * the primary rays repeat), halved into the previous value */
+        uint32_t* const tc = tile_cost + ty * tilesX + tx;
+        const uint64_t c = (__builtin_amdgcn_s_memtime() - c0) >> 1;
+        *tc = (*tc >> 1) + (c > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)c);
+    }
 #if WCPT_MK_TIMERS
     if (!COUNT && (threadIdx.x & 63u) == 0u)
         for (int k = 0; k < kPhaseTimers; k++) atomicAdd(&counters[k], (unsigned long long)cnt.tim[k]);
@@ -380,10 +392,91 @@ static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stre
         while (gcd(m, tiles) != 1u) m += 2u;
         scatter = m;
     }
+    /* cost-ordered tiles (auto order, render launches): this render records every tile's time, and the renders after
+     * a sort (launch_megakernel) take the tiles longest first */
+    const bool cost_order = !COUNT && a.mk_tile_order == 2 && mk.cost != nullptr;
     hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE>), dim3(tiles), dim3(64), 0, stream, a.sd,
                        a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H, a.y0,
-                       a.rows, tilesX, tiles, scatter, a.status, a.counters);
+                       a.rows, tilesX, tiles, scatter, cost_order && mk.order_valid ? mk.order : nullptr,
+                       cost_order ? mk.cost : nullptr, a.status, a.counters);
     return hipGetLastError();
+}
+
+__global__ void fill_iota(uint32_t* __restrict__ v, uint32_t n)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = i;
+}
+
+void mk_release(MkState& mk)
+{
+    if (mk.mem) (void)hipFree(mk.mem);
+    const int cus = mk.cus;
+    mk = MkState{};
+    mk.cus = cus;
+}
+
+/* Longest-first tile order from the costs the renders record (tile time in shader cycles). Measured (round 3,
+ * tools/tile_trace.py, 20 frames x 4 interleaved rounds): tile times vary with a coefficient of variation of 0.5-0.66
+ * across a frame and repeat from frame to frame for a still camera (the same primary rays); starting the longest
+ * tiles first leaves the short ones to fill the launch's last round: the Cornell box 0.3863 -> 0.3761 ms, its
+ * 270-row block 0.1251 -> 0.1209 ms, the reference's scene 1.486 -> 1.284 ms. Sorted after the first render of a
+ * geometry, after its 4th and 16th and then every kResortEvery renders (a radix sort of one key per tile, ~tens of
+ * microseconds). */
+constexpr uint32_t kResortEvery = 64;
+static hipError_t cost_order_prepare(const LaunchArgs& a, MkState& mk, uint32_t tiles, hipStream_t stream)
+{
+    if (tiles > mk.cap) {
+        if (mk.mem) {
+            hipError_t e = hipStreamSynchronize(stream);
+            if (e != hipSuccess) return e;
+            (void)hipFree(mk.mem);
+            mk.mem = nullptr;
+            mk.cap = 0;
+        }
+        size_t temp = 0;
+        hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr,
+                                                                    (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                                                    (uint32_t*)nullptr, (int)tiles, 0, 32, stream);
+        if (e != hipSuccess) return e;
+        const size_t words = 4ull * tiles;
+        const size_t bytes = ((words * 4ull + 255ull) & ~255ull) + temp;
+        void* m = nullptr;
+        e = hipMalloc(&m, bytes);
+        if (e != hipSuccess) return e;
+        mk.mem = m;
+        uint32_t* u = static_cast<uint32_t*>(m);
+        mk.cost = u;
+        mk.keys = u + tiles;
+        mk.iota = u + 2ull * tiles;
+        mk.order = u + 3ull * tiles;
+        mk.temp = static_cast<char*>(m) + ((words * 4ull + 255ull) & ~255ull);
+        mk.temp_bytes = temp;
+        mk.cap = tiles;
+        mk.geom_tiles = 0; /* forces the reset below */
+    }
+    if (mk.geom_tiles != tiles || mk.geom_w != a.W || mk.geom_rows != a.rows || mk.geom_y0 != a.y0) {
+        mk.geom_tiles = tiles;
+        mk.geom_w = a.W;
+        mk.geom_rows = a.rows;
+        mk.geom_y0 = a.y0;
+        mk.renders = 0;
+        mk.order_valid = false;
+        return hipMemsetAsync(mk.cost, 0, (size_t)tiles * 4u, stream); /* the running averages start at 0 */
+    }
+    return hipSuccess;
+}
+
+static hipError_t cost_order_sort(MkState& mk, uint32_t tiles, hipStream_t stream)
+{
+    hipLaunchKernelGGL(fill_iota, dim3(std::min<uint32_t>((tiles + 255u) / 256u, 1024u)), dim3(256), 0, stream,
+                       mk.iota, tiles);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t temp = mk.temp_bytes;
+    e = hipcub::DeviceRadixSort::SortPairsDescending(mk.temp, temp, mk.cost, mk.keys, mk.iota, mk.order, (int)tiles, 0,
+                                                     32, stream);
+    if (e == hipSuccess) mk.order_valid = true;
+    return e;
 }
 
 template <bool PAIRS, bool SINGLE>
@@ -412,14 +505,25 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
         if (e == hipSuccess) e = hipDeviceGetAttribute(&mk.cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
     }
+    const bool cost_order = mode == kModeRender && a.mk_tile_order == 2;
+    if (cost_order) {
+        hipError_t e = cost_order_prepare(a, mk, tiles, stream);
+        if (e != hipSuccess) return e;
+    }
     /* one draw command (the reference's case): the single-draw instantiation, without the draw loop */
     const bool single = a.sd.drawCommandCount == 1u;
-    if (a.pair_records) {
-        if (single) return launch_mega_sk<true, true>(a, mode, stack_kind, mk, stream, tilesX, tiles);
-        return launch_mega_sk<true, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
-    }
-    if (single) return launch_mega_sk<false, true>(a, mode, stack_kind, mk, stream, tilesX, tiles);
-    return launch_mega_sk<false, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    hipError_t e;
+    if (a.pair_records)
+        e = single ? launch_mega_sk<true, true>(a, mode, stack_kind, mk, stream, tilesX, tiles)
+                   : launch_mega_sk<true, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    else
+        e = single ? launch_mega_sk<false, true>(a, mode, stack_kind, mk, stream, tilesX, tiles)
+                   : launch_mega_sk<false, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    if (e != hipSuccess || !cost_order) return e;
+    /* sorted after renders 1, 4 and 16 of a geometry (the running averages settle), then every kResortEvery */
+    const uint32_t r = ++mk.renders;
+    if (r == 1u || r == 4u || r == 16u || r % kResortEvery == 0u) return cost_order_sort(mk, tiles, stream);
+    return hipSuccess;
 }
 
 hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint32_t* out, uint32_t n, hipStream_t stream)

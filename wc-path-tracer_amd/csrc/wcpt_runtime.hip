@@ -133,7 +133,7 @@ struct wcpt_context {
     uint32_t* d_status = nullptr;
     unsigned long long* d_counters = nullptr;
     wcpt::WfPipes wf;                  /* path state + streams of the wavefront pipelines (allocated on first use) */
-    wcpt::MkState mk;                  /* megakernel launch state (CU count) */
+    wcpt::MkState mk;                  /* megakernel launch state (CU count, cost-ordered tiles) */
     uint32_t* d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
@@ -578,6 +578,7 @@ int wcpt_destroy(wcpt_context* ctx)
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     wcpt::wf_release(ctx->wf);
+    wcpt::mk_release(ctx->mk);
     for (auto& t : ctx->tri) {
         if (t.mem) (void)hipFree(t.mem);
         if (t.pmem) (void)hipFree(t.pmem);
