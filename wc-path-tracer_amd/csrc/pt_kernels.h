@@ -28,6 +28,8 @@ struct LaunchArgs {
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
+    bool wf_fast;                /* wavefront trace: draw 0 has packed stack refs, 24-bit record offsets and a known
+                                    node count (table flags 1|2, word 2 high half > 0) */
     uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto, 3-6 striped bands (WCPT_OPTION_MK_TILE_ORDER) */
     float4* image;
     float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
@@ -78,7 +80,7 @@ struct WfState {
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     int cus = 0;                   /* compute units of the context's device (0 = not yet queried)          */
-    int trace_bpc[3][2][3] = {};   /* trace-kernel blocks per CU by (mode, single draw, LDS stack variant)  */
+    int trace_bpc[3][3][3] = {};   /* trace-kernel blocks per CU by (mode, geometry variant, LDS stack)      */
 };
 
 /* Concurrent wavefront pipelines (WCPT_OPTION_WF_PIPES): pipeline j of K owns the 8x8 tiles t with t % K == j and

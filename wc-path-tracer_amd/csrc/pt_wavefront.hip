@@ -104,6 +104,12 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_ANYHIT_LAST
 #define WCPT_WF_ANYHIT_LAST 1
 #endif
+#ifndef WCPT_WF_POP_ONCE
+#define WCPT_WF_POP_ONCE 1
+#endif
+#ifndef WCPT_WF_GEO2_WAVES
+#define WCPT_WF_GEO2_WAVES 8 /* occupancy floor of the fast-layout trace (waves per SIMD) */
+#endif
 
 /* ---- ray generation ------------------------------------------------------------------------------- */
 template <bool COUNT>
@@ -173,6 +179,9 @@ enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 
 #ifndef WCPT_WF_PAIR_RSRC
 #define WCPT_WF_PAIR_RSRC 1
 #endif
+#ifndef WCPT_WF_GEO_FAST
+#define WCPT_WF_GEO_FAST 1
+#endif
 struct Geom {
     gtri_ptr tris;
     uint32_t ntri;
@@ -229,8 +238,11 @@ __device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, const
     mode = count > 0 ? kModeLeaf : kModeInterior;
 }
 
-template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
-__global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
+/* GEO: 0 any draws; 1 one draw command (the reference's case, kernel-uniform geometry in scalar registers); 2 one draw
+ * whose table flags allow packed stack refs, 24-bit record offsets and buffer-resource node loads (the host checks
+ * them), so the loop carries no branches for the other layouts. */
+template <bool COUNT, bool DIAG, int GEO, int LDSN>
+__global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
                                                   const wcpt_draw_command* __restrict__ draws,
                                                   const uint64_t* __restrict__ tri_records, WfBuffers b,
                                                   uint32_t* __restrict__ status, unsigned long long* __restrict__ counters,
@@ -248,7 +260,12 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     Counters cnt = {};
     bool overflow = false;
     Geom g0 = {}, gl = g0;
+    constexpr bool SINGLE = GEO >= 1;
     if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
+    if (GEO == 2) {
+        g0.packed = true;
+        g0.idx24 = true;
+    }
 
     bool has = false, drained = false;
     /* this wave's claimed queue range [lo, hi) (wave-uniform). The first chunk is static (chunk blockIdx.x), so a
@@ -272,8 +289,9 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
     uint64_t t_drain = 0; /* DIAG: when this wave found the queue empty (its tail starts) */
 
     /* Start draw command d, or the next one whose root survives the cull (:152-162); kModeDone past the last. */
+    const uint32_t ndraw = SINGLE ? 1u : sd.drawCommandCount; /* SINGLE: the host launched it for one draw */
     auto start_draw = [&]() {
-        for (; d < sd.drawCommandCount; d++) {
+        for (; d < ndraw; d++) {
             if (!SINGLE) gl = load_geom(draws, tri_records, d);
             const Geom& g = SINGLE ? g0 : gl;
             if (COUNT) { cnt.draw_fetches++; cnt.node_pops++; }
@@ -353,6 +371,26 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
              * its first triangle in the same iteration (measured 1.4% faster than leaf -> interior -> pop). Each
              * lane still executes exactly the reference's sequence of steps. */
             if (has && mode == kModePop) {
+#if WCPT_WF_POP_ONCE
+                /* one stack entry per iteration: a culled entry (:162) leaves the lane in pop mode */
+                if (stk.empty()) {
+                    if (SINGLE) {
+                        mode = kModeDone; /* the only draw is done */
+                    } else {
+                        d++;
+                        start_draw();
+                    }
+                } else {
+                    uint32_t ni;
+                    float t0;
+                    stk.pop(ni, t0);
+                    ref_pop<COUNT>(rf);
+                    if (!(t0 > rt)) {
+                        const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
+                        cursor_from(lc.x, lc.y, g, ca, cb, cr, mode);
+                    }
+                }
+#else
                 bool found = false;
                 while (!stk.empty()) {
                     uint32_t ni;
@@ -369,16 +407,10 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                     d++;
                     start_draw();
                 }
+#endif
             }
-            diag_mark<DIAG>(tim, tprev, 3); /* pop */
-            if (has && mode == kModeInterior) {
-                NodeV L, R;
-                if (WCPT_WF_PAIR_RSRC && g.nodes) {
-                    load_pair_rsrc(g.rsrc, ca, L, R);
-                } else {
-                    L = load_node(g.bvh, ca);
-                    R = load_node(g.bvh, ca + 1);
-                }
+            /* the interior step on the fetched child pair (:164-200) */
+            auto interior_step = [&](const NodeV& L, const NodeV& R) {
                 float l0, l1, r0, r1;
                 node_box(ray, L, l0, l1);
                 node_box(ray, R, r0, r1);
@@ -410,14 +442,9 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 } else {
                     mode = kModePop;
                 }
-            }
-            diag_mark<DIAG>(tim, tprev, 2);
-            if (has && mode == kModeLeaf) {
-                /* one triangle per step, from the single records (pair records measured slower here: most
-                 * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
-                const TriE tr = cr != kNoRecord ? load_tri_at(g.tris, cr)
-                                                : tri_from_indices(g.indices, g.vertices, ca,
-                                                                   draw_vertex_count(tri_records, SINGLE ? 0u : d));
+            };
+            /* one triangle of the leaf (:174-190) */
+            auto leaf_step = [&](const TriE& tr) {
                 const float tt = rayTriangleE(ray, tr.a, tr.e1, tr.e2);
                 if (COUNT) {
                     cnt.triangle_tests++;
@@ -433,6 +460,26 @@ __global__ __launch_bounds__(64, wf_waves_per_simd(LDSN)) void wf_trace(const wc
                 cr += (cr != kNoRecord) ? 48u : 0u;
                 if (ca >= cb) mode = kModePop;
                 if (acc && any) mode = kModeDone; /* any-hit segment: its answer is fixed */
+            };
+            auto index_tri = [&]() {
+                return tri_from_indices(g.indices, g.vertices, ca, draw_vertex_count(tri_records, SINGLE ? 0u : d));
+            };
+            diag_mark<DIAG>(tim, tprev, 3); /* pop */
+            if (has && mode == kModeInterior) {
+                NodeV L, R;
+                if (WCPT_WF_PAIR_RSRC && (GEO == 2 || g.nodes)) {
+                    load_pair_rsrc(g.rsrc, ca, L, R);
+                } else {
+                    L = load_node(g.bvh, ca);
+                    R = load_node(g.bvh, ca + 1);
+                }
+                interior_step(L, R);
+            }
+            diag_mark<DIAG>(tim, tprev, 2);
+            if (has && mode == kModeLeaf) {
+                /* one triangle per step, from the single records (pair records measured slower here: most
+                 * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
+                leaf_step(cr != kNoRecord ? load_tri_at(g.tris, cr) : index_tri());
             }
             diag_mark<DIAG>(tim, tprev, 1);
             if (has && mode == kModeDone) {
@@ -683,43 +730,53 @@ __global__ __launch_bounds__(256) void wf_sort_keys(WfBuffers b, uint32_t P, con
     }
 }
 
-template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
+template <bool COUNT, bool DIAG, int GEO, int LDSN>
 static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace_grid, uint32_t shade_grid,
                          hipStream_t stream)
 {
-    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
+    hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, GEO, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
                        a.tri_records, b, a.status, a.counters, a.wf_refill);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
                        a.spheres, a.draws, a.tri_records, b, a.image, a.W, a.H, a.y0, a.counters);
 }
 
-template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
+template <bool COUNT, bool DIAG, int GEO, int LDSN>
 static hipError_t trace_blocks_per_cu(int& bpc)
 {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<COUNT, DIAG, SINGLE, LDSN>, 64, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<COUNT, DIAG, GEO, LDSN>, 64, 0);
 }
 
 /* One (mode, single-draw, LDS depth) instantiation: occupancy query or one trace+shade iteration. */
-template <bool COUNT, bool DIAG, bool SINGLE, int LDSN>
+template <bool COUNT, bool DIAG, int GEO, int LDSN>
 static hipError_t wf_variant(bool query, int& bpc, const LaunchArgs& a, const WfBuffers& b, uint32_t trace_grid,
                              uint32_t shade_grid, hipStream_t stream)
 {
-    if (query) return trace_blocks_per_cu<COUNT, DIAG, SINGLE, LDSN>(bpc);
-    wf_iteration<COUNT, DIAG, SINGLE, LDSN>(a, b, trace_grid, shade_grid, stream);
+    if (query) return trace_blocks_per_cu<COUNT, DIAG, GEO, LDSN>(bpc);
+    wf_iteration<COUNT, DIAG, GEO, LDSN>(a, b, trace_grid, shade_grid, stream);
     return hipGetLastError();
 }
 
-static hipError_t wf_dispatch(int mode, bool single, int ldsn, bool query, int& bpc, const LaunchArgs& a,
+static hipError_t wf_dispatch(int mode, int geo, int ldsn, bool query, int& bpc, const LaunchArgs& a,
                               const WfBuffers& b, uint32_t tg, uint32_t sg, hipStream_t st)
 {
-    if (mode == kModeCount) return single ? wf_variant<true, false, true, 10>(query, bpc, a, b, tg, sg, st)
-                                          : wf_variant<true, false, false, 10>(query, bpc, a, b, tg, sg, st);
-    if (mode == kModeDiag) return single ? wf_variant<true, true, true, 10>(query, bpc, a, b, tg, sg, st)
-                                         : wf_variant<true, true, false, 10>(query, bpc, a, b, tg, sg, st);
-    if (!single) return wf_variant<false, false, false, 10>(query, bpc, a, b, tg, sg, st);
-    if (ldsn == 16) return wf_variant<false, false, true, 16>(query, bpc, a, b, tg, sg, st);
-    if (ldsn == 24) return wf_variant<false, false, true, 24>(query, bpc, a, b, tg, sg, st);
-    return wf_variant<false, false, true, 10>(query, bpc, a, b, tg, sg, st);
+    const bool single = geo >= 1;
+    if (mode == kModeCount) return single ? wf_variant<true, false, 1, 10>(query, bpc, a, b, tg, sg, st)
+                                          : wf_variant<true, false, 0, 10>(query, bpc, a, b, tg, sg, st);
+    if (mode == kModeDiag) return single ? wf_variant<true, true, 1, 10>(query, bpc, a, b, tg, sg, st)
+                                         : wf_variant<true, true, 0, 10>(query, bpc, a, b, tg, sg, st);
+    if (!single) return wf_variant<false, false, 0, 10>(query, bpc, a, b, tg, sg, st);
+    if (geo == 2) return wf_variant<false, false, 2, 10>(query, bpc, a, b, tg, sg, st);
+    if (ldsn == 16) return wf_variant<false, false, 1, 16>(query, bpc, a, b, tg, sg, st);
+    if (ldsn == 24) return wf_variant<false, false, 1, 24>(query, bpc, a, b, tg, sg, st);
+    return wf_variant<false, false, 1, 10>(query, bpc, a, b, tg, sg, st);
+}
+
+/* The trace instantiation for this launch: 0 any draws, 1 one draw, 2 one draw on the fast layout (render build, the
+ * default LDS stack; LaunchArgs::wf_fast). */
+static int wf_geo(const LaunchArgs& a, int mode, int ldsn)
+{
+    if (a.sd.drawCommandCount != 1) return 0;
+    return (WCPT_WF_GEO_FAST && a.wf_fast && mode == kModeRender && ldsn == 10) ? 2 : 1;
 }
 
 static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b, uint32_t P, int cus,
@@ -786,7 +843,7 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
     const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
     if (pipe >= tiles) return hipSuccess;
     const uint32_t P = min(((tiles - pipe + npipes - 1u) / npipes) * 64u, a.W * a.rows); /* as pipe_begin */
-    const bool single = a.sd.drawCommandCount == 1; /* the reference's case (PathTracingRenderer.jai:251) */
+    const int geo = wf_geo(a, mode, ldsn); /* one draw: the reference's case (PathTracingRenderer.jai:251) */
     hipError_t e = hipSuccess;
     /* each iteration advances every live path by one segment; a path needs <= samples*(maxBounce+1) */
     uint64_t iters = (uint64_t)a.sd.samples * ((uint64_t)a.sd.maxBounceCount + 1ull);
@@ -799,7 +856,7 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
             b.order = s.sort_order;
         }
         int unused = 0;
-        e = wf_dispatch(mode, single, ldsn, false, unused, a, b, trace_grid, shade_grid, stream);
+        e = wf_dispatch(mode, geo, ldsn, false, unused, a, b, trace_grid, shade_grid, stream);
         if (e != hipSuccess) return e;
         std::swap(b.in, b.out);
         std::swap(b.count_in, b.count_out);
@@ -819,11 +876,11 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     int cus = 0;
     hipError_t e = cu_count(s0, cus);
     if (e != hipSuccess) return e;
-    const bool single = a.sd.drawCommandCount == 1;
     const int ldsn = (lds_stack == 16 || lds_stack == 24) ? lds_stack : 10;
-    int& bpc = s0.trace_bpc[mode][single ? 1 : 0][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
+    const int geo = wf_geo(a, mode, ldsn);
+    int& bpc = s0.trace_bpc[mode][geo][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
     if (bpc == 0) {
-        e = wf_dispatch(mode, single, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);
+        e = wf_dispatch(mode, geo, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);
         if (e != hipSuccess) return e;
         if (bpc < 1) bpc = 1;
     }

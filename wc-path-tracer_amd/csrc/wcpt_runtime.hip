@@ -257,6 +257,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
 {
     const uint32_t n = sd.drawCommandCount;
     a.tri_records = nullptr;
+    a.wf_fast = false;
     if (n == 0) return WCPT_SUCCESS;
     std::vector<wcpt_draw_command> dc(n);
     const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
@@ -342,6 +343,8 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         tris_max = std::max<uint64_t>(tris_max, ntri);
         leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
     }
+    /* the wavefront trace's one-draw fast layout: packed stack refs, 24-bit record offsets, buffer-resource node loads */
+    a.wf_fast = n == 1 && (ctx->tri_table[3] & 3u) == 3u && (ctx->tri_table[2] >> 32) > 0;
     /* pair leaves address a draw's pair records with 32-bit byte offsets (pt_device.h load_pair_at) */
     a.pair_records = tris_max <= kPairMaxTriangles &&
                      (ctx->pair_records == 1 ||
@@ -441,6 +444,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.counters = ctx->d_counters;
     a.tri_records = nullptr;
     a.pair_records = false;
+    a.wf_fast = false;
     a.wf_refill = (uint32_t)ctx->wf_refill;
     a.mk_tile_order = (uint32_t)ctx->mk_tile_order;
     hipEvent_t e0 = nullptr, e1 = nullptr;
