@@ -721,6 +721,15 @@ __device__ __forceinline__ uint32_t leaf_record_off24(uint32_t first, uint32_t c
     const bool aligned = (mul_u32_u24(first, 0xAAAAABu) & 0xFFFFFFu) <= 0x555555u;
     return (aligned && first <= lim3 && count <= lim3 - first) ? first * 16u : kNoRecord;
 }
+/* The single record of the triangle at index position `pos` (the reference reads indices pos..pos+2, :174-176) as a
+ * byte offset, for kTriFlagIndex24 draws: record k = pos / 3 was derived from exactly those indices when pos is a
+ * multiple of 3 and k < ntri (pos < lim3 = 3 * ntri); else kNoRecord (the index path). Per triangle, so a leaf's
+ * cursor needs no record offset of its own. */
+__device__ __forceinline__ uint32_t tri_record_off24(uint32_t pos, uint32_t lim3)
+{
+    const bool aligned = (mul_u32_u24(pos, 0xAAAAABu) & 0xFFFFFFu) <= 0x555555u;
+    return (aligned && pos < lim3) ? pos * 16u : kNoRecord;
+}
 /* leaf_record as a byte offset for any draw (records beyond 4 GiB take the index path) */
 __device__ __forceinline__ uint32_t leaf_record_off(uint32_t first, uint32_t count, uint32_t ntri)
 {
@@ -1234,6 +1243,9 @@ __device__ __forceinline__ bool interior_step(const Ray& ray, const DrawGeom& g,
     return false;
 }
 
+#ifndef WCPT_MK_POP_ONCE
+#define WCPT_MK_POP_ONCE 1
+#endif
 /* Pop (:157-162): the next deferred node whose box entry distance is not beyond rec.t; false when none is left. */
 template <bool COUNT, class Stack>
 __device__ __forceinline__ bool pop_step(const DrawGeom& g, Stack& stk, uint32_t& curLeft, uint32_t& curCount, float rt,
@@ -1331,9 +1343,30 @@ __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& 
             mode = curCount > 0 ? kLeaf : kInterior;
         }
         while (mode != kDone) {
+#if WCPT_MK_POP_ONCE
+            if (mode == kPop) {
+                /* one stack entry per iteration (no inner pop loop): a culled entry (:162) keeps the lane popping */
+                if (stk.empty()) {
+                    mode = kDone;
+                } else {
+                    uint32_t ni;
+                    float t0;
+                    stk.pop(ni, t0);
+                    ref_pop<COUNT>(rf);
+                    if (!(t0 > rt)) {
+                        const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
+                        curLeft = lc.x;
+                        curCount = lc.y;
+                        mode = curCount > 0 ? kLeaf : kInterior;
+                    }
+                }
+                phase_mark(cnt, 2);
+            }
+#else
             if (mode == kPop)
                 mode = pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf) ? (curCount > 0 ? kLeaf : kInterior)
                                                                                 : kDone;
+#endif
             if (mode == kInterior)
                 mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)
                            ? (curCount > 0 ? kLeaf : kInterior) : kPop;

@@ -228,13 +228,14 @@ __device__ __forceinline__ void diag_mark(uint64_t* tim, uint64_t& tprev, int k)
 }
 
 /* Node cursor: interior -> (a = left child index); leaf -> (a = current index position, b = end position,
- * r = byte offset of the current triangle's single record or kNoRecord). */
+ * r = byte offset of the current triangle's single record or kNoRecord; draws without kTriFlagIndex24 only). */
 __device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, const Geom& g, uint32_t& a, uint32_t& b,
                                             uint32_t& r, uint32_t& mode)
 {
     a = left;
     b = left + count;
-    r = g.idx24 ? leaf_record_off24(left, count, g.lim3) : leaf_record_off(left, count, g.ntri);
+    /* 24-bit draws find each triangle's record in the leaf step (tri_record_off24) */
+    r = g.idx24 ? 0u : leaf_record_off(left, count, g.ntri);
     mode = count > 0 ? kModeLeaf : kModeInterior;
 }
 
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                     primDraw = d;
                 }
                 ca += 3;
-                cr += (cr != kNoRecord) ? 48u : 0u;
+                if (!g.idx24) cr += (cr != kNoRecord) ? 48u : 0u;
                 if (ca >= cb) mode = kModePop;
                 if (acc && any) mode = kModeDone; /* any-hit segment: its answer is fixed */
             };
@@ -479,7 +480,8 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             if (has && mode == kModeLeaf) {
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
-                leaf_step(cr != kNoRecord ? load_tri_at(g.tris, cr) : index_tri());
+                const uint32_t off = g.idx24 ? tri_record_off24(ca, g.lim3) : cr;
+                leaf_step(off != kNoRecord ? load_tri_at(g.tris, off) : index_tri());
             }
             diag_mark<DIAG>(tim, tprev, 1);
             if (has && mode == kModeDone) {
