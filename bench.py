@@ -58,8 +58,8 @@ DEFAULT_KERNEL = {"c1": wcpt.KERNEL_MEGAKERNEL, "c2": wcpt.KERNEL_MEGAKERNEL, "c
 # 2.4 GHz peak engine clock (tools/valu_peak.hip measures it: profiles/r03_valu_peak.log)
 SIMDS = 1024
 CLOCK_GHZ = 2.4
-CYCLES_PER_VALU = 4
-VALU_PEAK_GCYCLES = SIMDS * CLOCK_GHZ  # issue cycles per ns over the chip
+CYCLES_PER_VALU = 2  # a wave64 VALU instruction issues over 2 cycles on the 32-lane SIMD (MI355X_MICROARCH.md)
+VALU_PEAK_GINSTR = SIMDS * CLOCK_GHZ / CYCLES_PER_VALU  # spec: 1,228.8 G wave64 VALU instructions/s
 
 
 def algorithmic_bytes(c: dict) -> int:
@@ -86,8 +86,9 @@ def roofline(args, tot, render_s, frame_s) -> dict:
     """The dominant kernel against the ceiling of the resource that binds it, measured per render.
 
     valu_issue (megakernel; c2): SQ_INSTS_VALU wave-instructions per render from the committed SQ counter pass
-      (profiles/sq_<config>.json) x 4 cycles each, over the live render time: G VALU issue-cycles/s against the chip's
-      1024 SIMDs x 2.4 GHz. frac = the share of the SIMDs' issue slots spent on VALU.
+      (profiles/sq_<config>.json) over the live render time, against the spec issue rate (1024 SIMDs x 2.4 GHz, one
+      wave64 instruction per 2 cycles); measured_ceiling = the rate the kernel's VALU instruction mix could reach
+      (profiles/valu_mix_<config>.json x profiles/valu_ceiling.json).
     memory_latency (wavefront trace; c3): dependent scene-line visits (one 64-B child pair per interior visit, one
       triangle record per test) per second of the frame, against the best rate of dependent random line visits the
       cache hierarchy sustains at 8 waves/SIMD (L2-resident chain, tools/gather_bench.hip, profiles/gather_ceiling.json).
@@ -110,15 +111,15 @@ def roofline(args, tot, render_s, frame_s) -> dict:
     bound = None if sq is None else sq.get("bound")
     if bound == "valu_issue":
         valu = sq["counters_per_launch"]["SQ_INSTS_VALU"] * sq.get("launches_per_frame", 1.0)
-        achieved = valu * CYCLES_PER_VALU / render_s / 1e9
-        head = {"bound": "valu_issue", "achieved": round(achieved, 1), "peak": VALU_PEAK_GCYCLES,
-                "unit": "G VALU issue-cycles/s", "frac": round(achieved / VALU_PEAK_GCYCLES, 3),
-                "source": f"SQ_INSTS_VALU {valu:.4g}/render ({sq.get('source', 'profiles')}) x {CYCLES_PER_VALU} "
-                          f"cycles over the live render time; peak {SIMDS} SIMDs x {CLOCK_GHZ} GHz"}
-        ceil = _json_field("valu_ceiling.json", "issue_gcycles_per_s")
+        achieved = valu / render_s / 1e9
+        head = {"bound": "valu_issue", "achieved": round(achieved, 1), "peak": VALU_PEAK_GINSTR,
+                "unit": "G wave64 VALU instructions/s", "frac": round(achieved / VALU_PEAK_GINSTR, 3),
+                "source": f"SQ_INSTS_VALU {valu:.4g}/render ({sq.get('source', 'profiles')}) over the live render "
+                          f"time; peak {SIMDS} SIMDs x {CLOCK_GHZ} GHz / {CYCLES_PER_VALU} cycles"}
+        ceil = _valu_mix_ceiling(args.config)
         if ceil:
-            # the best VALU rate measured on the chip (independent FMA chains, 8 waves/SIMD): the clock under load
-            # sits below the 2.4 GHz spec, so this is the attainable ceiling
+            # what this kernel's VALU mix can reach: each instruction class at the fastest rate measured for an
+            # instruction of that class (tools/valu_peak.hip; v_add/v_mul/v_mov issue about twice as fast as v_fma)
             head["measured_ceiling"] = ceil
             head["measured_frac"] = round(achieved / ceil, 3)
     elif bound == "memory_latency":
@@ -143,6 +144,19 @@ def _json_field(name: str, key: str):
     try:
         return float(json.load(open(os.path.join(ROOT, "profiles", name)))[key])
     except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def _valu_mix_ceiling(config: str):
+    """Mix-weighted VALU ceiling (G wave64 instructions/s) of the config's dominant kernel: 1 / sum(f_c / R_c) over the
+    instruction classes c of profiles/valu_mix_<config>.json (fractions f_c of SQ_INSTS_VALU) with the class rates R_c
+    of profiles/valu_ceiling.json."""
+    try:
+        rates = json.load(open(os.path.join(ROOT, "profiles", "valu_ceiling.json")))["class_gwave_instr_per_s"]
+        mix = json.load(open(os.path.join(ROOT, "profiles", f"valu_mix_{config}.json")))["class_fraction"]
+        t = sum(f / float(rates[c]) for c, f in mix.items() if f > 0)
+        return round(1.0 / t, 1) if t > 0 else None
+    except (OSError, ValueError, KeyError, TypeError, ZeroDivisionError):
         return None
 
 

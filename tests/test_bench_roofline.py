@@ -1,0 +1,68 @@
+"""bench.py's roofline object on CPU: the committed profiles (profiles/sq_*.json, valu_mix_*.json, valu_ceiling.json,
+pmc_traffic_*.json) priced the way the bench line prices them, with the round-3 render times. Every fraction of a
+binding resource must stay <= 1: a kernel cannot beat the ceiling it is priced against."""
+import argparse
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _args(config, kernel):
+    return argparse.Namespace(steps=1, config=config, kernel=kernel, bvh="midpoint", pmc_json=None)
+
+
+def _counters(**kw):
+    c = dict(sphere_tests=0, node_pops=0, interior_visits=0, triangle_tests=0, hits=0, draw_fetches=0, pixels=0)
+    c.update(kw)
+    return c
+
+
+def _profile(name):
+    return json.load(open(os.path.join(ROOT, "profiles", name)))
+
+
+def test_valu_ceiling_classes_and_mix_ceiling():
+    ceil = _profile("valu_ceiling.json")
+    rates = ceil["class_gwave_instr_per_s"]
+    assert ceil["spec_gwave_instr_per_s"] == pytest.approx(bench.VALU_PEAK_GINSTR)
+    for cfg in ("c2", "ref", "c3"):
+        mix = _profile(f"valu_mix_{cfg}.json")["class_fraction"]
+        assert set(mix) <= set(rates)
+        assert sum(mix.values()) == pytest.approx(1.0, abs=1e-3)
+        m = bench._valu_mix_ceiling(cfg)
+        # a weighted harmonic mean of the class rates lies between the slowest and the fastest class used
+        used = [rates[c] for c, f in mix.items() if f > 0]
+        assert min(used) <= m <= max(used)
+
+
+@pytest.mark.parametrize("config,render_ms", [("c2", 0.3701), ("ref", 1.259)])
+def test_valu_roofline_fractions_at_most_one(config, render_ms):
+    sq = _profile(f"sq_{config}.json")
+    assert sq["bound"] == "valu_issue"
+    r = bench.roofline(_args(config, sq["kernel"]), _counters(pixels=1920 * 1080), render_ms * 1e-3, render_ms * 1e-3)
+    assert r["bound"] == "valu_issue" and r["unit"] == "G wave64 VALU instructions/s"
+    assert r["peak"] == pytest.approx(1228.8)
+    assert 0 < r["frac"] <= 1.0
+    assert 0 < r["measured_frac"] <= 1.0
+    assert r["measured_ceiling"] < r["peak"]
+    # the achieved rate is the committed VALU count over the render time
+    valu = sq["counters_per_launch"]["SQ_INSTS_VALU"]
+    assert r["achieved"] == pytest.approx(valu / (render_ms * 1e-3) / 1e9, rel=1e-3)
+    assert r["traffic"] is not None and 0 < r["hbm_measured_frac"] < 1.0
+
+
+def test_memory_latency_roofline_c3():
+    sq = _profile("sq_c3.json")
+    assert sq["bound"] == "memory_latency"
+    # one c3 frame's exact counts (round 3): 8.57 M segments, 453 M interior visits, 105 M triangle tests
+    tot = _counters(interior_visits=453249769, triangle_tests=104965350, node_pops=915070762, pixels=1920 * 1080)
+    r = bench.roofline(_args("c3", sq["kernel"]), tot, 4.97e-3, 4.97e-3)
+    assert r["bound"] == "memory_latency"
+    assert 0 < r["frac"] <= 1.0
+    assert r["algorithmic_note"].startswith("cache-served")

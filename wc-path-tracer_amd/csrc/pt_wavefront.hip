@@ -104,6 +104,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_ANYHIT_LAST
 #define WCPT_WF_ANYHIT_LAST 1
 #endif
+#ifndef WCPT_WF_TAIL_WINDOW
+#define WCPT_WF_TAIL_WINDOW 16 /* rays per wave of the grid: claims for idle lanes only in the queue's last window */
+#endif
 #ifndef WCPT_WF_POP_ONCE
 #define WCPT_WF_POP_ONCE 1
 #endif
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
         g0.idx24 = true;
     }
 
-    bool has = false, drained = false;
+    bool has = false, drained = false, tail_claims = false;
     /* this wave's claimed queue range [lo, hi) (wave-uniform). The first chunk is static (chunk blockIdx.x), so a
      * launch with fewer rays than resident waves costs no atomics for the waves without work: same-address
      * device-scope atomics serialise, and one per wave of the persistent grid cost ~0.28 ms per launch. Later
@@ -320,14 +323,18 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                         drained = true;
                         break;
                     }
-                    if (lane == 0) base = static_end + atomicAdd(b.head, kTraceChunk);
+                    /* near the end of the queue a wave claims only as many rays as it has idle lanes: a full chunk
+                     * there is a reserve that one wave works through alone while the others have drained */
+                    const uint32_t csz = tail_claims ? (uint32_t)__popcll(need) : kTraceChunk;
+                    if (lane == 0) base = static_end + atomicAdd(b.head, csz);
                     base = __builtin_amdgcn_readfirstlane(base); /* wave-uniform: keeps lo/hi in SGPRs */
                     if (base >= n) {
                         drained = true;
                         break;
                     }
                     lo = base;
-                    hi = min(base + kTraceChunk, n);
+                    hi = min(base + csz, n);
+                    tail_claims = WCPT_WF_TAIL_WINDOW > 0 && hi + gridDim.x * WCPT_WF_TAIL_WINDOW >= n;
                 }
                 const uint32_t avail = hi - lo;
                 const uint32_t rank = (uint32_t)__popcll(need & lanemask_lt());
