@@ -921,6 +921,9 @@ struct PrivateStack {
     }
 };
 
+#ifndef WCPT_STACK_UNIFORM_FAST
+#define WCPT_STACK_UNIFORM_FAST 0
+#endif
 /* Entries are packed (node index | t0 bits << 32). The two storage classes are typed by address space so that
  * the compiler emits ds_read/ds_write for the LDS part and scratch_* for the spill instead of merging the two
  * into one flat access. */
@@ -934,6 +937,15 @@ struct LdsStack {
     __device__ __forceinline__ bool push(uint32_t i, float t)
     {
         const uint64_t e = (uint64_t)i | ((uint64_t)__float_as_uint(t) << 32);
+#if WCPT_STACK_UNIFORM_FAST
+        /* wave-uniform fast path: no pushing lane has reached the spill region (one compare and a scalar branch
+         * instead of the exec-mask bookkeeping of a divergent if/else) */
+        if (!__ballot(sp >= N)) {
+            base[sp * 64] = e;
+            sp++;
+            return true;
+        }
+#endif
         if (sp < N) {
             base[sp * 64] = e;
         } else if (sp < N + SPILL) {
@@ -948,6 +960,11 @@ struct LdsStack {
     {
         sp--;
         uint64_t e;
+#if WCPT_STACK_UNIFORM_FAST
+        if (!__ballot(sp >= N)) {
+            e = base[sp * 64];
+        } else
+#endif
         if (sp < N)
             e = base[sp * 64];
         else
