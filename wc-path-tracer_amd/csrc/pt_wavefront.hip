@@ -334,7 +334,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                     }
                     lo = base;
                     hi = min(base + csz, n);
-                    tail_claims = WCPT_WF_TAIL_WINDOW > 0 && hi + gridDim.x * WCPT_WF_TAIL_WINDOW >= n;
+                    tail_claims = WCPT_WF_TAIL_WINDOW > 0 && (uint64_t)hi + (uint64_t)gridDim.x * WCPT_WF_TAIL_WINDOW >= n;
                 }
                 const uint32_t avail = hi - lo;
                 const uint32_t rank = (uint32_t)__popcll(need & lanemask_lt());
