@@ -66,3 +66,13 @@ def test_memory_latency_roofline_c3():
     assert r["bound"] == "memory_latency"
     assert 0 < r["frac"] <= 1.0
     assert r["algorithmic_note"].startswith("cache-served")
+
+
+def test_c4_profiles_priced_per_frame():
+    # c4 (3840x2160, 16 spp): 2 pipelines x 80 trace launches per frame; the PMC traffic is whole-frame
+    sq = _profile("sq_c4.json")
+    assert sq["bound"] == "memory_latency" and sq["launches_per_frame"] == 160.0
+    assert sq["counters_per_launch"]["SQ_WAVES"] > 0
+    r = bench.roofline(_args("c4", sq["kernel"]), _counters(pixels=3840 * 2160), 0.2612, 0.2612)
+    assert r["traffic"] == _profile("pmc_traffic_c4.json")["hbm_bytes_per_frame"]
+    assert 0 < r["hbm_measured_frac"] < 1.0
