@@ -56,6 +56,7 @@ struct WfBuffers {
     PathSoA out;       /* queue shade appends the continuing paths to                   */
     float4* hit;       /* by input slot: (t, primitive bits, draw bits, -) of Intersect */
     float4* result;    /* by pixel: sum of sample radiance .xyz                          */
+    float4* prim_hit;  /* by pixel: the primary segment's Intersect record (sample 0), reused by samples 1.. */
     const uint32_t* order; /* optional trace order of the input slots (ray sorting), or null */
     uint32_t* count_in;
     uint32_t* count_out;
@@ -91,7 +92,7 @@ constexpr int kWfMaxPipes = 4;
 struct WfPipes {
     WfState pipe[kWfMaxPipes];
     float4* result = nullptr;            /* by pixel: sum of sample radiance .xyz (all pipelines) */
-    uint64_t result_capacity = 0;        /* pixels */
+    uint64_t result_capacity = 0;        /* pixels; `result` holds 2 x this many float4: the sums, then prim_hit */
     hipStream_t aux[kWfMaxPipes] = {};   /* [1..K-1]: created on first use, on the context's device */
     hipEvent_t fork = nullptr;
     hipEvent_t join[kWfMaxPipes] = {};

@@ -110,6 +110,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_POP_ONCE
 #define WCPT_WF_POP_ONCE 1
 #endif
+#ifndef WCPT_WF_PRIMARY_REUSE
+#define WCPT_WF_PRIMARY_REUSE 1 /* samples 1.. shade their primary segment from sample 0's record */
+#endif
 #ifndef WCPT_WF_GEO2_WAVES
 #define WCPT_WF_GEO2_WAVES 8 /* occupancy floor of the fast-layout trace (waves per SIMD) */
 #endif
@@ -539,41 +542,61 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
             ps.bounce = __float_as_uint(r1.z);
             sample = __float_as_uint(r1.w);
             seed = __float_as_uint(li.w);
-            const uint32_t prim = __float_as_uint(hi.y);
-            const Hit h = resolve_hit(ps.ray, hi.x, prim, __float_as_uint(hi.z), spheres, draws, tri_records);
-            if (COUNT && h.hit) cnt.hits++;
-            f3 L;
-            if (!path_shade(ps, h, seed, sd, mats, L, sample + 1u == sd.samples)) {
-                cont = true;
-            } else {
-                const float4 rs = b.result[p];
-                f3 result = mk3(rs.x, rs.y, rs.z) + L;                    /* :310 */
+            /* Every sample of a pixel starts with the same primary ray (:302, :309-310), so its Intersect record is
+             * the same too: sample 0's is kept by pixel and later samples shade their primary segment from it
+             * without tracing it again (render build only: the COUNT build traces every segment, as the reference
+             * does, for the exact counters). */
+            const bool reuse = !COUNT && WCPT_WF_PRIMARY_REUSE && sd.samples > 1u;
+            if (reuse && ps.bounce == 0u && sample == 0u) b.prim_hit[p] = hi;
+            float4 h4 = hi;
+            f3 result = mk3(0.0f, 0.0f, 0.0f);
+            bool summed = false; /* result holds b.result[p] + this call's finished samples */
+            for (;;) {
+                const Hit h = resolve_hit(ps.ray, h4.x, __float_as_uint(h4.y), __float_as_uint(h4.z), spheres, draws,
+                                          tri_records);
+                if (COUNT && h.hit) cnt.hits++;
+                f3 L;
+                if (!path_shade(ps, h, seed, sd, mats, L, sample + 1u == sd.samples)) {
+                    cont = true;
+                    break;
+                }
+                if (!summed) {
+                    const float4 rs = b.result[p];
+                    result = mk3(rs.x, rs.y, rs.z);
+                    summed = true;
+                }
+                result = result + L;                                           /* :310 */
                 sample++;
                 const uint32_t lx = p % W, ly = p / W;
                 if (sample < sd.samples) {                                  /* next sample, same primary ray */
                     path_begin(ps, mk3(sd.position[0], sd.position[1], sd.position[2]),
                                primary_direction(sd, lx, y0 + ly, W, H));
-                    b.result[p] = make_float4(result.x, result.y, result.z, 0.0f);
-                    cont = true;
-                } else {
-                    result = result / (float)sd.samples;                   /* :312 */
-                    if (!COUNT) {
-                        float4* px = image + (size_t)ly * W + lx;
-                        f3 acc;
-                        if (sd.renderedFramesCount == 0) {
-                            acc = result;
-                        } else {
-                            const float4 o = *px;
-                            const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u);
-                            const float iw = 1.0f - weight;
-                            acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight,
-                                      o.z * iw + result.z * weight);
-                        }
-                        store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, acc); /* :323 */
+                    if (!reuse) {
+                        cont = true;
+                        break;
                     }
-                    if (COUNT) cnt.pixels++;
+                    h4 = b.prim_hit[p];
+                    continue;
                 }
+                result = result / (float)sd.samples;                       /* :312 */
+                if (!COUNT) {
+                    float4* px = image + (size_t)ly * W + lx;
+                    f3 acc;
+                    if (sd.renderedFramesCount == 0) {
+                        acc = result;
+                    } else {
+                        const float4 o = *px;
+                        const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u);
+                        const float iw = 1.0f - weight;
+                        acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight,
+                                  o.z * iw + result.z * weight);
+                    }
+                    store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, acc); /* :323 */
+                }
+                if (COUNT) cnt.pixels++;
+                break;
             }
+            if (cont && summed) b.result[p] = make_float4(result.x, result.y, result.z, 0.0f);
             if (cont) segment_prologue<COUNT>(ps.ray, sd, spheres, rt0, prim0, cnt);
         }
         const uint32_t slot = block_append(b.count_out, cont, s_wave, &s_base);
@@ -671,7 +694,7 @@ static hipError_t wf_reserve_result(WfPipes& w, uint64_t pixels)
     if (w.result) (void)hipFree(w.result);
     w.result = nullptr;
     w.result_capacity = 0;
-    hipError_t e = hipMalloc(&w.result, pixels * sizeof(float4));
+    hipError_t e = hipMalloc(&w.result, 2 * pixels * sizeof(float4)); /* the sums, then the primary records */
     if (e != hipSuccess) return e;
     w.result_capacity = pixels;
     return hipSuccess;
@@ -805,7 +828,7 @@ static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b
 
 /* One pipeline: init (pipe_begin) + samples*(maxBounce+1) trace/shade iterations (pipe_iterate) over the tiles t with
  * t % npipes == pipe. */
-static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, float4* result,
+static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const WfState& s0, float4* result, float4* prim_hit,
                              uint32_t pipe, uint32_t npipes, int cus, hipStream_t stream, WfBuffers& b)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
@@ -822,6 +845,7 @@ static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const Wf
     b.in = s.soa[0];
     b.out = s.soa[1];
     b.result = result;
+    b.prim_hit = prim_hit;
     b.hit = s.hit;
     b.order = nullptr;
     b.head = s.ctr + 2;
@@ -854,8 +878,11 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
     const uint32_t P = min(((tiles - pipe + npipes - 1u) / npipes) * 64u, a.W * a.rows); /* as pipe_begin */
     const int geo = wf_geo(a, mode, ldsn); /* one draw: the reference's case (PathTracingRenderer.jai:251) */
     hipError_t e = hipSuccess;
-    /* each iteration advances every live path by one segment; a path needs <= samples*(maxBounce+1) */
+    /* each iteration advances every live path by one traced segment; a path needs <= samples*(maxBounce+1), or
+     * with the primary records reused (wf_shade) maxBounce+1 for sample 0 and maxBounce for each later sample */
     uint64_t iters = (uint64_t)a.sd.samples * ((uint64_t)a.sd.maxBounceCount + 1ull);
+    if (WCPT_WF_PRIMARY_REUSE && mode == kModeRender && a.sd.samples > 1u)
+        iters = (uint64_t)a.sd.maxBounceCount + 1ull + (uint64_t)(a.sd.samples - 1u) * a.sd.maxBounceCount;
     if (iters > (1ull << 20)) iters = 1ull << 20; /* bounded; WCPT documents the cap */
     for (uint64_t it = 0; it < iters; it++) {
         b.order = nullptr;
@@ -920,7 +947,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     if (e != hipSuccess) return e;
     WfBuffers bs[kWfMaxPipes];
     if (K == 1) {
-        e = pipe_begin(a, mode, s0, s0, w.result, 0, 1, cus, stream, bs[0]);
+        e = pipe_begin(a, mode, s0, s0, w.result, w.result + w.result_capacity, 0, 1, cus, stream, bs[0]);
         if (e != hipSuccess) return e;
         return pipe_iterate(a, mode, s0, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream, bs[0]);
     }
@@ -948,7 +975,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     }
     hipError_t first = hipSuccess;
     for (uint32_t j = 0; j < K && first == hipSuccess; j++)
-        first = pipe_begin(a, mode, w.pipe[j], s0, w.result, j, K, cus, j == 0 ? stream : w.aux[j], bs[j]);
+        first = pipe_begin(a, mode, w.pipe[j], s0, w.result, w.result + w.result_capacity, j, K, cus, j == 0 ? stream : w.aux[j], bs[j]);
 #ifndef WCPT_WF_START_TOGETHER
 #define WCPT_WF_START_TOGETHER 0
 #endif
