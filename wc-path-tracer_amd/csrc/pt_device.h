@@ -1310,119 +1310,133 @@ __device__ __forceinline__ bool root_step(const Ray& ray, const DrawGeom& g, flo
  * form -- a loop over draws containing the divergent traversal loops, inside the divergent bounce loop -- is
  * mis-compiled by this toolchain whenever the traversal grows (a DIAG build or the scalar-load leaf loop on the
  * atrium overflowed the stack, tools/stack_probe.py), while this flat form is not. */
+/* Every sample of a pixel starts with the same primary ray (pathTracer.comp:302, :309-310), so its Intersect record is
+ * the same too: the megakernel keeps sample 0's and later samples resolve their primary segment from it (render
+ * builds for samples > 1 only, a separate instantiation -- keeping the record costs the one-sample kernel 20 VGPRs --
+ * and never the COUNT build, which traces every segment as the reference does for the exact counters). */
+#ifndef WCPT_MK_PRIMARY_REUSE
+#define WCPT_MK_PRIMARY_REUSE 1
+#endif
 template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
 __device__ __forceinline__ Hit intersect(const Ray& ray, const wcpt_scene_data& sd, const wcpt_sphere* __restrict__ spheres,
                                          const wcpt_draw_command* __restrict__ draws,
                                          const uint64_t* __restrict__ tri_records, Stack& stk,
-                                         Counters& cnt, bool& overflow, bool primary)
+                                         Counters& cnt, bool& overflow, bool primary, float4& prim_rec,
+                                         bool reuse_primary)
 {
     float rt = kInfinity;
     uint32_t prim = kNoPrim, primDraw = 0;
-    if (COUNT) {
-        cnt.segments++;
-        simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
-    }
+    if (!COUNT && WCPT_MK_PRIMARY_REUSE && reuse_primary) { /* a later sample's primary segment (TraceRay) */
+        rt = prim_rec.x;
+        prim = __float_as_uint(prim_rec.y);
+        primDraw = __float_as_uint(prim_rec.z);
+    } else {
+        if (COUNT) {
+            cnt.segments++;
+            simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
+        }
 
-    sphere_loop(ray, sd.sphereCount, spheres, rt, prim);
-    if (COUNT) cnt.sphere_tests += sd.sphereCount;
+        sphere_loop(ray, sd.sphereCount, spheres, rt, prim);
+        if (COUNT) cnt.sphere_tests += sd.sphereCount;
 #if WCPT_DUP_SPHERES
-    {
-        Ray r2 = ray;
-        r2.origin.x = launder(r2.origin.x);
-        r2.direction.x = launder(r2.direction.x);
-        float rt2 = kInfinity;
-        uint32_t p2 = 0;
-        for (uint32_t i = 0; i < sd.sphereCount; i++) {
-            const wcpt_sphere& s = spheres[i];
-            const float tr = raySphereNear(r2, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
-            if (tr > 0.0f && tr < rt2) { rt2 = tr; p2 = i; }
+        {
+            Ray r2 = ray;
+            r2.origin.x = launder(r2.origin.x);
+            r2.direction.x = launder(r2.direction.x);
+            float rt2 = kInfinity;
+            uint32_t p2 = 0;
+            for (uint32_t i = 0; i < sd.sphereCount; i++) {
+                const wcpt_sphere& s = spheres[i];
+                const float tr = raySphereNear(r2, mk3(s.position[0], s.position[1], s.position[2]), s.radius);
+                if (tr > 0.0f && tr < rt2) { rt2 = tr; p2 = i; }
+            }
+            sink(rt2);
+            sink_u(p2);
         }
-        sink(rt2);
-        sink_u(p2);
-    }
 #endif
-    phase_mark(cnt, 1);
+        phase_mark(cnt, 1);
 
-    uint32_t curLeft = 0, curCount = 0;
-    PeelCache pc;
-    pc.tag = kNoPeel;
-    pc.t = bc2(0.0f);
-    RefStack rf;
-    if constexpr (SINGLE) {
-        const DrawGeom g = draw_geom<PAIRS>(draws, tri_records, 0);
-        /* one traversal step per iteration as sequential ifs on the lane's mode (pop -> interior -> leaf), like
-         * wf_trace: a lane that pops an interior node visits it in the same iteration, one that descends into a
-         * leaf tests it in the same iteration */
-        enum : uint32_t { kInterior = 0, kLeaf = 1, kPop = 2, kDone = 3 };
-        uint32_t mode = kDone;
-        if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt, rf)) {
-            stk.reset();
-            mode = curCount > 0 ? kLeaf : kInterior;
-        }
-        while (mode != kDone) {
+        uint32_t curLeft = 0, curCount = 0;
+        PeelCache pc;
+        pc.tag = kNoPeel;
+        pc.t = bc2(0.0f);
+        RefStack rf;
+        if constexpr (SINGLE) {
+            const DrawGeom g = draw_geom<PAIRS>(draws, tri_records, 0);
+            /* one traversal step per iteration as sequential ifs on the lane's mode (pop -> interior -> leaf), like
+             * wf_trace: a lane that pops an interior node visits it in the same iteration, one that descends into a
+             * leaf tests it in the same iteration */
+            enum : uint32_t { kInterior = 0, kLeaf = 1, kPop = 2, kDone = 3 };
+            uint32_t mode = kDone;
+            if (sd.drawCommandCount != 0u && root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt, rf)) {
+                stk.reset();
+                mode = curCount > 0 ? kLeaf : kInterior;
+            }
+            while (mode != kDone) {
 #if WCPT_MK_POP_ONCE
-            if (mode == kPop) {
-                /* one stack entry per iteration (no inner pop loop): a culled entry (:162) keeps the lane popping */
-                if (stk.empty()) {
-                    mode = kDone;
-                } else {
-                    uint32_t ni;
-                    float t0;
-                    stk.pop(ni, t0);
-                    ref_pop<COUNT>(rf);
-                    if (!(t0 > rt)) {
-                        const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
-                        curLeft = lc.x;
-                        curCount = lc.y;
-                        mode = curCount > 0 ? kLeaf : kInterior;
+                if (mode == kPop) {
+                    /* one stack entry per iteration (no inner pop loop): a culled entry (:162) keeps the lane popping */
+                    if (stk.empty()) {
+                        mode = kDone;
+                    } else {
+                        uint32_t ni;
+                        float t0;
+                        stk.pop(ni, t0);
+                        ref_pop<COUNT>(rf);
+                        if (!(t0 > rt)) {
+                            const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
+                            curLeft = lc.x;
+                            curCount = lc.y;
+                            mode = curCount > 0 ? kLeaf : kInterior;
+                        }
+                    }
+                    phase_mark(cnt, 2);
+                }
+#else
+                if (mode == kPop)
+                    mode = pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf) ? (curCount > 0 ? kLeaf : kInterior)
+                                                                                    : kDone;
+#endif
+                if (mode == kInterior)
+                    mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)
+                               ? (curCount > 0 ? kLeaf : kInterior) : kPop;
+                if (mode == kLeaf) {
+                    leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
+                    mode = kPop;
+                }
+            }
+        } else {
+            uint32_t d = 0;
+            DrawGeom g;
+            float rt_before = rt;
+            /* first draw (from d on) whose root survives the cull */
+            auto start_draw = [&]() {
+                for (; d < sd.drawCommandCount; d++) {
+                    g = draw_geom<PAIRS>(draws, tri_records, d);
+                    rt_before = rt;
+                    if (root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt, rf)) {
+                        stk.reset();
+                        pc.tag = kNoPeel; /* offsets of another draw's records */
+                        return true;
                     }
                 }
-                phase_mark(cnt, 2);
-            }
-#else
-            if (mode == kPop)
-                mode = pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf) ? (curCount > 0 ? kLeaf : kInterior)
-                                                                                : kDone;
-#endif
-            if (mode == kInterior)
-                mode = interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)
-                           ? (curCount > 0 ? kLeaf : kInterior) : kPop;
-            if (mode == kLeaf) {
-                leaf_step<COUNT, DIAG, PAIRS, true>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
-                mode = kPop;
-            }
-        }
-    } else {
-        uint32_t d = 0;
-        DrawGeom g;
-        float rt_before = rt;
-        /* first draw (from d on) whose root survives the cull */
-        auto start_draw = [&]() {
-            for (; d < sd.drawCommandCount; d++) {
-                g = draw_geom<PAIRS>(draws, tri_records, d);
-                rt_before = rt;
-                if (root_step<COUNT>(ray, g, rt, curLeft, curCount, cnt, rf)) {
-                    stk.reset();
-                    pc.tag = kNoPeel; /* offsets of another draw's records */
-                    return true;
+                return false;
+            };
+            bool active = start_draw();
+            while (active) {
+                if (curCount > 0) {
+                    leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
+                } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)) {
+                    continue;
                 }
+                if (pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf)) continue;
+                if (rt != rt_before) primDraw = d; /* this draw lowered rt: it owns prim */
+                d++;
+                active = start_draw();
             }
-            return false;
-        };
-        bool active = start_draw();
-        while (active) {
-            if (curCount > 0) {
-                leaf_step<COUNT, DIAG, PAIRS, false>(ray, g, curLeft, curCount, rt, prim, cnt, primary, pc);
-            } else if (interior_step<COUNT, DIAG>(ray, g, stk, curLeft, curCount, rt, cnt, overflow, rf)) {
-                continue;
-            }
-            if (pop_step<COUNT>(g, stk, curLeft, curCount, rt, cnt, rf)) continue;
-            if (rt != rt_before) primDraw = d; /* this draw lowered rt: it owns prim */
-            d++;
-            active = start_draw();
         }
     }
-
+    if (!COUNT && WCPT_MK_PRIMARY_REUSE && primary && sd.samples > 1u) prim_rec = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
     if (COUNT && prim != kNoPrim) cnt.hits++;
     ref_segment_end<COUNT>(cnt);
     const Hit hit = resolve_hit(ray, rt, prim, primDraw, spheres, draws, tri_records);
@@ -1588,13 +1602,16 @@ __device__ __forceinline__ bool path_shade(PathState& ps, const Hit& h, uint32_t
     return false;
 }
 
-/* pathTracer.comp:241-284 */
-template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
+/* pathTracer.comp:241-284. prim_rec: the primary segment's Intersect record (t, primitive, draw), written by the
+ * first sample; reuse_primary: a later sample, whose primary segment reads it instead of tracing the same ray again
+ * (intersect). */
+template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack, bool REUSE = false>
 __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_data& sd,
                                        const wcpt_material* __restrict__ mats, const wcpt_sphere* __restrict__ spheres,
                                        const wcpt_draw_command* __restrict__ draws,
                                        const uint64_t* __restrict__ tri_records, Stack& stk,
-                                       Counters& cnt, bool& overflow, bool lastSample)
+                                       Counters& cnt, bool& overflow, bool lastSample, float4& prim_rec,
+                                       bool reuse_primary)
 {
     PathState ps;
     path_begin(ps, ray.origin, ray.direction);
@@ -1603,7 +1620,7 @@ __device__ __forceinline__ f3 TraceRay(Ray ray, uint32_t& rng, const wcpt_scene_
      * (segment 0: origin = the camera) is a wave-uniform branch condition */
     for (uint32_t seg = 0;; seg++) {
         const Hit h = intersect<COUNT, DIAG, PAIRS, SINGLE>(ps.ray, sd, spheres, draws, tri_records, stk, cnt, overflow,
-                                                           seg == 0u);
+                                                           seg == 0u, prim_rec, REUSE && seg == 0u && reuse_primary);
         const bool done = path_shade(ps, h, rng, sd, mats, L, lastSample);
         phase_mark(cnt, 5);
         if (done) return L;

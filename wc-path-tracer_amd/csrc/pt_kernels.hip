@@ -64,7 +64,7 @@ __device__ __forceinline__ void tile_of_block(uint32_t tilesX, uint32_t tilesTot
 }
 
 /* Shade one pixel (pathTracer.comp:290-323) with the given traversal stack. */
-template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, class Stack>
+template <bool COUNT, bool DIAG, bool PAIRS, bool SINGLE, bool REUSE, class Stack>
 __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcpt_material* __restrict__ mats,
                                             const wcpt_sphere* __restrict__ spheres,
                                             const wcpt_draw_command* __restrict__ draws,
@@ -85,13 +85,14 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
     phase_mark(cnt, 0);
     f3 result = mk3(0.0f, 0.0f, 0.0f);
     const f3 origin = mk3(sd.position[0], sd.position[1], sd.position[2]);
+    float4 prim_rec = make_float4(0.0f, 0.0f, 0.0f, 0.0f); /* sample 0's primary Intersect record */
     for (uint32_t s = 0; s < sd.samples; s++) { /* :309-310, all samples share the primary ray */
         Ray r;
         r.origin = origin;
         r.direction = dir;
         r.invDirection = rcp3(dir);
-        result = result + TraceRay<COUNT, DIAG, PAIRS, SINGLE>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow,
-                                                       s + 1u == sd.samples);
+        result = result + TraceRay<COUNT, DIAG, PAIRS, SINGLE, Stack, REUSE>(r, seed, sd, mats, spheres, draws, tri_records, stk, cnt, overflow,
+                                                       s + 1u == sd.samples, prim_rec, s > 0u);
     }
     result = result / (float)sd.samples; /* :312 */
     if (!COUNT) {
@@ -116,7 +117,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
 #ifndef WCPT_MK_WAVES
 #define WCPT_MK_WAVES 1
 #endif
-template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE>
+template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE, bool REUSE>
 __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                     const wcpt_sphere* __restrict__ spheres,
                                                     const wcpt_draw_command* __restrict__ draws,
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
             uint64_t mem[kPrivateStack];
             PrivateStack<kPrivateStack> stk;
             stk.mem = (priv_u64_ptr)mem;
-            shade_pixel<COUNT, DIAG, PAIRS, SINGLE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
+            shade_pixel<COUNT, DIAG, PAIRS, SINGLE, REUSE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
                                             cnt, overflow);
         } else {
             __shared__ uint64_t s_stack[kLdsStack * 64];
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
             LdsStack<kLdsStack, kSpillStack> stk;
             stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
             stk.spill = (priv_u64_ptr)spill;
-            shade_pixel<COUNT, DIAG, PAIRS, SINGLE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
+            shade_pixel<COUNT, DIAG, PAIRS, SINGLE, REUSE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
                                             cnt, overflow);
         }
     }
@@ -374,7 +375,7 @@ hipError_t launch_build_primary_pairs(const void* pairs, uint32_t npairs, float 
     return hipGetLastError();
 }
 
-template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE>
+template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE, bool REUSE = false>
 static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
 {
     /* scattered tile order: block b renders tile (b * m) mod tiles for an m coprime with tiles near 0.618 * tiles,
@@ -395,7 +396,7 @@ static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stre
     /* cost-ordered tiles (auto order, render launches): this render records every tile's time, and the renders after
      * a sort (launch_megakernel) take the tiles longest first */
     const bool cost_order = !COUNT && a.mk_tile_order == 2 && mk.cost != nullptr;
-    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE>), dim3(tiles), dim3(64), 0, stream, a.sd,
+    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE, REUSE>), dim3(tiles), dim3(64), 0, stream, a.sd,
                        a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H, a.y0,
                        a.rows, tilesX, tiles, scatter, cost_order && mk.order_valid ? mk.order : nullptr,
                        cost_order ? mk.cost : nullptr, a.status, a.counters);
@@ -484,11 +485,17 @@ static hipError_t launch_mega_sk(const LaunchArgs& a, int mode, int stack_kind, 
                                  uint32_t tilesX, uint32_t tiles)
 {
     if (stack_kind == 0) {
-        if (mode == kModeRender) return launch_mega<false, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+        if (mode == kModeRender)
+            return a.sd.samples > 1u && WCPT_MK_PRIMARY_REUSE
+                       ? launch_mega<false, false, 0, PAIRS, SINGLE, true>(a, mk, stream, tilesX, tiles)
+                       : launch_mega<false, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
         if (mode == kModeCount) return launch_mega<true, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
         return launch_mega<true, true, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
     }
-    if (mode == kModeRender) return launch_mega<false, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+    if (mode == kModeRender)
+        return a.sd.samples > 1u && WCPT_MK_PRIMARY_REUSE
+                   ? launch_mega<false, false, 1, PAIRS, SINGLE, true>(a, mk, stream, tilesX, tiles)
+                   : launch_mega<false, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
     if (mode == kModeCount) return launch_mega<true, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
     return launch_mega<true, true, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
 }
