@@ -124,12 +124,20 @@ def roofline(args, tot, render_s, frame_s) -> dict:
             head["measured_frac"] = round(achieved / ceil, 3)
     elif bound == "memory_latency":
         ceil = _gather_ceiling()
-        lines = (tot["interior_visits"] + tot["triangle_tests"]) / steps
+        # the line visits the kernels execute: with samples > 1 every sample after the first shades its primary
+        # segment from sample 0's Intersect record (the same ray), so those traversals are counted by the reference's
+        # work (COUNT build) but never run, and are taken out here
+        reused = tot.get("reused_primary_lines", 0)
+        lines = (tot["interior_visits"] + tot["triangle_tests"] - reused) / steps
         achieved = lines / frame_s / 1e9
         head = {"bound": "memory_latency", "achieved": round(achieved, 2), "peak": ceil,
                 "unit": "G dependent line-visits/s", "frac": round(achieved / ceil, 3),
-                "source": "interior visits + triangle tests per frame over the frame time; peak: dependent random "
-                          "64-B line visits at 8 waves/SIMD from an L2-resident table (profiles/gather_ceiling.json)"}
+                "source": "interior visits + triangle tests executed per frame over the frame time (the reference's "
+                          "counts less the primary traversals of samples after the first, which reuse sample 0's "
+                          "record); peak: dependent random 64-B line visits at 8 waves/SIMD from an L2-resident "
+                          "table (profiles/gather_ceiling.json)"}
+        if reused:
+            head["reused_primary_lines_per_frame"] = int(reused / steps)
     else:
         head = {"bound": "unprofiled", "achieved": None, "peak": None, "unit": None, "frac": None,
                 "source": f"no SQ counter pass committed for {args.config} (profiles/sq_{args.config}.json)"}
@@ -439,6 +447,11 @@ def main():
         c = ctx.render_counters(sdk, *addrs)
         for n in tot:
             tot[n] = max(tot[n], c[n]) if n == "ref_stack_max" else tot[n] + c[n]
+    if spp > 1:
+        # primary segments (samples = 1, no bounce): the same rays every sample of a frame traces first; the render
+        # traces them once per pixel and samples 1..spp-1 reuse that record (pt_wavefront.hip wf_shade, pt_device.h)
+        cp = ctx.render_counters(scene.scene_data(W, H, max_bounce=0, samples=1, frame=args.warmup), *addrs)
+        tot["reused_primary_lines"] = (spp - 1) * (cp["interior_visits"] + cp["triangle_tests"]) * args.steps
     if world > 1:
         t = torch.tensor([elapsed, float(tot["segments"]), float(tot["pixels"] * spp)], dtype=torch.float64,
                          device="cpu" if host_staged else "cuda")
