@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--rows", type=int, default=0, help="render rows [0, rows) only (a row block of an N-way split)")
+    ap.add_argument("--check", action="store_true", help="compare the variants' last images bit for bit")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
@@ -57,6 +58,7 @@ def main():
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
     segs = sum(ctx.render_counters(sd, *scenes["0"].addresses())["segments"] for sd in sds)
     res = {v: [] for v in a.variants}
+    imgs = {}
     for r in range(a.rounds + 1):
         for v in a.variants:
             o = parse(v)
@@ -77,10 +79,17 @@ def main():
             ctx.sync()
             if r > 0:
                 res[v].append(ms / n)
+            if a.check and r == a.rounds:
+                imgs[v] = ctx.readback(a.rows or H).view(np.uint32).copy()
     print(f"{a.config}: {desc}; {segs / a.frames:.0f} segments/frame")
     for v, t in res.items():
         m = statistics.median(t)
         print(f"  {v:30s} {m:8.3f} ms/frame  {segs / a.frames / m / 1e3:9.1f} Mray/s   (runs {', '.join(f'{x:.3f}' for x in t)})")
+    if imgs:
+        first = next(iter(imgs.values()))
+        for v, im in imgs.items():
+            print(f"  image of {v}: {'bit-identical to' if np.array_equal(im, first) else 'DIFFERS from'} "
+                  f"{a.variants[0]} ({int((im != first).any(axis=-1).sum())} pixels differ)")
     for d in scenes.values():
         d.free()
     ctx.close()
