@@ -560,6 +560,9 @@ __device__ __forceinline__ v2f bc2(float s) { v2f r = {s, s}; return r; }
  * the reference's acceptance test (t > 0, u, v, u + v in range). A triangle is taken iff it passed and t < rec.t;
  * that equals the reference's `t != -1 && t < rec.t` on its -1-for-miss result (a pass implies t > 0). */
 struct PairHit { v2f t; bool hit0, hit1; };
+#ifndef WCPT_PAIR_PIN
+#define WCPT_PAIR_PIN 1
+#endif
 __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& p)
 {
     const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
@@ -569,14 +572,21 @@ __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& 
     const v2f py = dz * p.e2x - p.e2z * dx;
     const v2f pz = dx * p.e2y - p.e2x * dy;
     const v2f det = (p.e1x * px + p.e1y * py) + p.e1z * pz;
-    const v2f inv = rcp2_exact(det);
     /* crossROAE1 = cross(oa, e1) */
     const v2f qx = oay * p.e1z - p.e1y * oaz;
     const v2f qy = oaz * p.e1x - p.e1z * oax;
     const v2f qz = oax * p.e1y - p.e1x * oay;
-    const v2f u = ((oax * px + oay * py) + oaz * pz) * inv;
+    const v2f un = (oax * px + oay * py) + oaz * pz; /* dot(oa, crossRDE2) */
+    const v2f tn = (p.e2x * qx + p.e2y * qy) + p.e2z * qz; /* dot(edgeAC, crossROAE1) */
+#if WCPT_PAIR_PIN
+    /* computed before the reciprocal: its fallback branch would otherwise split the block, and these independent
+     * products would be sunk past it instead of filling the det -> rcp -> Newton chain's dependency stalls */
+    asm volatile("" ::"v"(qx), "v"(qy), "v"(qz), "v"(un), "v"(tn));
+#endif
+    const v2f inv = rcp2_exact(det);
+    const v2f u = un * inv;
     const v2f v = (dx * (qx * inv) + dy * (qy * inv)) + dz * (qz * inv);
-    const v2f t = ((p.e2x * qx + p.e2y * qy) + p.e2z * qz) * inv;
+    const v2f t = tn * inv;
     const v2f uv = u + v;
     PairHit h;
     h.t = t;
