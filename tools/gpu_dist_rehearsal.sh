@@ -21,4 +21,6 @@ run n2_c2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --m
     --master-port 29510 bench.py --gpus 2 --config c2 --steps 5 --warmup 2 --dist-backend gloo --verify || exit 1
 run n2_c3 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29530 bench.py --gpus 2 --config c3 --steps 3 --warmup 1 --dist-backend gloo --verify || exit 1
+run n2_c4 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29540 bench.py --gpus 2 --config c4 --steps 2 --warmup 1 --dist-backend gloo --verify || exit 1
 echo ALL_DONE
