@@ -69,10 +69,26 @@ def test_memory_latency_roofline_c3():
 
 
 def test_c4_profiles_priced_per_frame():
-    # c4 (3840x2160, 16 spp): 2 pipelines x 80 trace launches per frame; the PMC traffic is whole-frame
+    # c4 (3840x2160, 16 spp, 4 bounces): 2 pipelines x 65 trace launches per frame -- 5 segments for sample 0 and 4 for
+    # each later sample, whose primary segment reuses sample 0's record; the PMC traffic is whole-frame
     sq = _profile("sq_c4.json")
-    assert sq["bound"] == "memory_latency" and sq["launches_per_frame"] == 160.0
+    assert sq["bound"] == "memory_latency" and sq["launches_per_frame"] == 2 * (5 + 15 * 4)
     assert sq["counters_per_launch"]["SQ_WAVES"] > 0
     r = bench.roofline(_args("c4", sq["kernel"]), _counters(pixels=3840 * 2160), 0.2612, 0.2612)
     assert r["traffic"] == _profile("pmc_traffic_c4.json")["hbm_bytes_per_frame"]
     assert 0 < r["hbm_measured_frac"] < 1.0
+
+
+def test_memory_latency_roofline_takes_out_reused_primary_visits():
+    # with samples > 1 the render traces each pixel's primary ray once; the reference's counts (COUNT build) include
+    # the other samples' primary traversals, which bench.py passes as reused_primary_lines and prices out
+    sq = _profile("sq_c4.json")
+    tot = _counters(interior_visits=30_000_000_000, triangle_tests=5_000_000_000, pixels=3840 * 2160)
+    full = bench.roofline(_args("c4", sq["kernel"]), dict(tot), 0.2121, 0.2121)
+    tot["reused_primary_lines"] = 8_000_000_000
+    r = bench.roofline(_args("c4", sq["kernel"]), tot, 0.2121, 0.2121)
+    assert r["reused_primary_lines_per_frame"] == 8_000_000_000
+    assert r["achieved"] == pytest.approx(full["achieved"] * (35 - 8) / 35, rel=1e-3)
+    assert 0 < r["frac"] < full["frac"] <= 1.0
+    # the algorithmic (reference-work) bytes are not reduced: they price the reference's traversal
+    assert r["algorithmic_bytes_per_render"] == full["algorithmic_bytes_per_render"]
