@@ -353,6 +353,10 @@ __device__ __forceinline__ uint2 node_ref_lc(bool packed, gnode_ptr bvh, uint32_
     if ((ref & 255u) != kRefFetch) return make_uint2(ref >> 8, ref & 255u);
     return load_node_lc(bvh, ref >> 8);
 }
+/* The packed forms when every index and count fits (the wavefront fast layout: < 2^24 nodes and index positions,
+ * every triangleCount < kRefFetch, kTriFlagSmallLeaves): no fetch case */
+__device__ __forceinline__ uint32_t node_ref_small(uint32_t left, uint32_t count) { return (left << 8) | count; }
+__device__ __forceinline__ uint2 node_ref_lc_small(uint32_t ref) { return make_uint2(ref >> 8, ref & 255u); }
 __device__ __forceinline__ void node_box(const Ray& r, const NodeV& n, float& t0, float& t1)
 {
     /* node = {min.xyz, max.x | max.yz, left, count} */
@@ -486,6 +490,8 @@ __device__ __forceinline__ float rayTriangle(const Ray& r, f3 a, f3 b, f3 c) { r
 constexpr uint32_t kTriTableWords = 5;
 constexpr uint64_t kTriFlagPackedRefs = 1u; /* table word 3: stack entries may carry (left, count) */
 constexpr uint64_t kTriFlagIndex24 = 2u;    /* table word 3: the draw's indexCount is < 2^24 */
+constexpr uint64_t kTriFlagSmallLeaves = 4u; /* table word 3: every node's triangleCount is < kRefFetch, so every packed
+                                                stack entry carries its node's (left, count) */
 /* table word 3, bits 32..63: vertices in the draw's vertex buffer (0xFFFFFFFF: unknown, not a context buffer) */
 __device__ __forceinline__ uint32_t draw_vertex_count(const uint64_t* __restrict__ tri_records, uint32_t draw)
 {

@@ -187,6 +187,14 @@ __device__ __forceinline__ void tri_fields(const uint32_t* __restrict__ idx, con
     f[6] = e2.x; f[7] = e2.y; f[8] = e2.z;
 }
 
+/* Sets *big when some leaf of the BVH has triangleCount >= kRefFetch (a stack entry of it would not carry its count). */
+__global__ __launch_bounds__(256) void scan_leaf_counts(const wcpt_node* __restrict__ bvh, uint32_t nodes,
+                                                        uint32_t* __restrict__ big)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < nodes && bvh[i].triangleCount >= kRefFetch) atomicOr(big, 1u);
+}
+
 __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restrict__ idx, const float* __restrict__ vtx,
                                                          uint32_t ntri, uint32_t nvert, float4* __restrict__ singles,
                                                          float4* __restrict__ out)
@@ -361,6 +369,15 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
     const uint32_t npairs = (uint32_t)((triangles + 1ull) / 2ull);
     hipLaunchKernelGGL(dev::build_tri_records, dim3((npairs + 255u) / 256u), dim3(256), 0, stream, indices, vertices,
                        triangles, vertex_count, static_cast<float4*>(singles), static_cast<float4*>(pairs));
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_leaf_counts(const void* bvh, uint32_t nodes, uint32_t* big, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(big, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess || nodes == 0) return e;
+    hipLaunchKernelGGL(dev::scan_leaf_counts, dim3((nodes + 255u) / 256u), dim3(256), 0, stream,
+                       static_cast<const wcpt_node*>(bvh), nodes, big);
     return hipGetLastError();
 }
 

@@ -113,6 +113,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_PRIMARY_REUSE
 #define WCPT_WF_PRIMARY_REUSE 1 /* samples 1.. shade their primary segment from sample 0's record */
 #endif
+#ifndef WCPT_WF_SMALL_LEAVES
+#define WCPT_WF_SMALL_LEAVES 1 /* the fast layout also requires kTriFlagSmallLeaves: packed stack entries need no fetch case */
+#endif
 #ifndef WCPT_WF_GEO2_WAVES
 #define WCPT_WF_GEO2_WAVES 8 /* occupancy floor of the fast-layout trace (waves per SIMD) */
 #endif
@@ -397,7 +400,8 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                     stk.pop(ni, t0);
                     ref_pop<COUNT>(rf);
                     if (!(t0 > rt)) {
-                        const uint2 lc = node_ref_lc(g.packed, g.bvh, ni);
+                        const uint2 lc = (GEO == 2 && WCPT_WF_SMALL_LEAVES) ? node_ref_lc_small(ni)
+                                                                            : node_ref_lc(g.packed, g.bvh, ni);
                         cursor_from(lc.x, lc.y, g, ca, cb, cr, mode);
                     }
                 }
@@ -443,7 +447,9 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 const float farT0 = leftFirst ? r0 : l0;
                 if (passFar && (COUNT || !WCPT_WF_PUSH_CULL || !(farT0 > rt))) {
                     const NodeV& F = leftFirst ? R : L;
-                    if (!stk.push(node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w), farT0))
+                    const uint32_t fref = (GEO == 2 && WCPT_WF_SMALL_LEAVES) ? node_ref_small(F.b.z, F.b.w)
+                                                                            : node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w);
+                    if (!stk.push(fref, farT0))
                         overflow = true;
                 }
                 ref_interior<COUNT>(rf, passFar, cnt); /* the counting build pushes every passing far child */

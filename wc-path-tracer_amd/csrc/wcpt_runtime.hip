@@ -79,6 +79,11 @@ struct TriRecords {
     uint64_t cap = 0;
     uint64_t pair_offset = 0;
     uint64_t build_id = 0;  /* incremented on every rebuild of the records */
+    /* whether every node of the draw's BVH (address bvh, `bvh_nodes` nodes, buffer generation gen_bvh) has
+     * triangleCount < 255 (pt_device.h kTriFlagSmallLeaves) */
+    uint64_t bvh = 0, gen_bvh = kUnknownGeneration;
+    uint64_t bvh_nodes = 0;
+    bool small_leaves = false, leaves_valid = false;
     /* primary-ray pair records (pt_device.h TriPairP) for the camera position `porigin` (bit patterns), derived from
      * the pair records of build `pbuild` */
     void* pmem = nullptr;
@@ -135,6 +140,7 @@ struct wcpt_context {
     wcpt::WfPipes wf;                  /* path state + streams of the wavefront pipelines (allocated on first use) */
     wcpt::MkState mk;                  /* megakernel launch state (CU count, cost-ordered tiles) */
     uint32_t* d_scratch = nullptr;
+    uint32_t* d_scan = nullptr;        /* leaf-count scan flag (prepare_tri_records) */
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
     int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + spill (default; c2 -2%, 135-row blocks -8%) */
@@ -328,6 +334,25 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         const uint64_t nodes = bb ? (bb->bytes - o) / sizeof(wcpt_node) : ~0ull;
         uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
         if (dc[d].indexCount < (1u << 24)) flags |= 2u; /* pt_device.h kTriFlagIndex24 */
+        if (flags & 1u) {
+            /* pt_device.h kTriFlagSmallLeaves: scanned on the device once per BVH buffer generation */
+            const uint64_t gb = bb->generation;
+            if (!(ctx->tri_cache && t.leaves_valid && t.bvh == dc[d].bvhBuffer && t.gen_bvh == gb && t.bvh_nodes == nodes)) {
+                if (!ctx->d_scan) HIP_TRY(ctx, hipMalloc(&ctx->d_scan, sizeof(uint32_t)), "hipMalloc(leaf scan flag)");
+                HIP_TRY(ctx, wcpt::launch_scan_leaf_counts(reinterpret_cast<const void*>(dc[d].bvhBuffer), (uint32_t)nodes,
+                                                           ctx->d_scan, ctx->stream), "scan_leaf_counts");
+                uint32_t big = 1;
+                HIP_TRY(ctx, hipMemcpyAsync(&big, ctx->d_scan, sizeof(big), hipMemcpyDeviceToHost, ctx->stream),
+                        "hipMemcpyAsync(leaf scan flag)");
+                HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(leaf scan flag)");
+                t.bvh = dc[d].bvhBuffer;
+                t.gen_bvh = gb;
+                t.bvh_nodes = nodes;
+                t.small_leaves = big == 0;
+                t.leaves_valid = true;
+            }
+            if (t.small_leaves) flags |= 4u;
+        }
         flags |= (uint64_t)nvert << 32;                 /* pt_device.h draw_vertex_count: bounds the index path */
         /* word 2: ntri, and in its high half the BVH node count when packed refs apply (the buffer-resource node loads
          * of pt_device.h load_pair_rsrc cover exactly those nodes) */
@@ -344,7 +369,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
     }
     /* the wavefront trace's one-draw fast layout: packed stack refs, 24-bit record offsets, buffer-resource node loads */
-    a.wf_fast = n == 1 && (ctx->tri_table[3] & 3u) == 3u && (ctx->tri_table[2] >> 32) > 0;
+    a.wf_fast = n == 1 && (ctx->tri_table[3] & 7u) == 7u && (ctx->tri_table[2] >> 32) > 0;
     /* pair leaves address a draw's pair records with 32-bit byte offsets (pt_device.h load_pair_at) */
     a.pair_records = tris_max <= kPairMaxTriangles &&
                      (ctx->pair_records == 1 ||
@@ -589,6 +614,7 @@ int wcpt_destroy(wcpt_context* ctx)
     }
     if (ctx->d_tri_table) (void)hipFree(ctx->d_tri_table);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->d_scan) (void)hipFree(ctx->d_scan);
     for (auto& p : ctx->events) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
