@@ -492,6 +492,9 @@ constexpr uint64_t kTriFlagPackedRefs = 1u; /* table word 3: stack entries may c
 constexpr uint64_t kTriFlagIndex24 = 2u;    /* table word 3: the draw's indexCount is < 2^24 */
 constexpr uint64_t kTriFlagSmallLeaves = 4u; /* table word 3: every node's triangleCount is < kRefFetch, so every packed
                                                 stack entry carries its node's (left, count) */
+constexpr uint64_t kTriFlagLeafRecords = 8u; /* table word 3: every leaf starts at a triangle boundary and ends within the
+                                                draw's derived records, so each leaf triangle at index position p is
+                                                single record p / 3 (byte offset 16 p) */
 /* table word 3, bits 32..63: vertices in the draw's vertex buffer (0xFFFFFFFF: unknown, not a context buffer) */
 __device__ __forceinline__ uint32_t draw_vertex_count(const uint64_t* __restrict__ tri_records, uint32_t draw)
 {

@@ -29,8 +29,8 @@ struct LaunchArgs {
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
     bool wf_fast;                /* wavefront trace: draw 0 has packed stack refs, 24-bit record offsets, leaves of < 255
-                                    index positions (kTriFlagSmallLeaves) and a known
-                                    node count (table flags 1|2|4, word 2 high half > 0) */
+                                    index positions on derived records (kTriFlagSmallLeaves, kTriFlagLeafRecords) and a known
+                                    node count (table flags 1|2|4|8, word 2 high half > 0) */
     uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto, 3-6 striped bands (WCPT_OPTION_MK_TILE_ORDER) */
     float4* image;
     float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
@@ -138,8 +138,10 @@ constexpr uint32_t kPrimPairRecordBytes = 112;
 /* Primary-ray pair records (pt_device.h TriPairP) of `npairs` pair records for the camera origin (ox, oy, oz). */
 hipError_t launch_build_primary_pairs(const void* pairs, uint32_t npairs, float ox, float oy, float oz, void* out,
                                       hipStream_t stream);
-/* *big (zeroed here) = 1 when some node of the BVH has triangleCount >= 255 (pt_device.h kRefFetch) */
-hipError_t launch_scan_leaf_counts(const void* bvh, uint32_t nodes, uint32_t* big, hipStream_t stream);
+/* *flags (zeroed here): bit 0 when some leaf of the BVH has triangleCount >= 255 (pt_device.h kRefFetch), bit 1 when
+ * some leaf's triangles are not all derived records of the draw's `triangles` (pt_device.h kTriFlagLeafRecords) */
+hipError_t launch_scan_leaf_counts(const void* bvh, uint32_t nodes, uint32_t triangles, uint32_t* flags,
+                                   hipStream_t stream);
 hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertices, uint32_t triangles,
                                     uint32_t vertex_count, void* singles, void* pairs, hipStream_t stream);
 /* composite.comp (pt_composite.hip): gamma + PBR Neutral over `pixels` float4 texels into rgba32f or RGBA8 */

@@ -187,12 +187,20 @@ __device__ __forceinline__ void tri_fields(const uint32_t* __restrict__ idx, con
     f[6] = e2.x; f[7] = e2.y; f[8] = e2.z;
 }
 
-/* Sets *big when some leaf of the BVH has triangleCount >= kRefFetch (a stack entry of it would not carry its count). */
-__global__ __launch_bounds__(256) void scan_leaf_counts(const wcpt_node* __restrict__ bvh, uint32_t nodes,
-                                                        uint32_t* __restrict__ big)
+/* The BVH's leaves against the fast layout's assumptions: *flags |= 1 when some leaf has triangleCount >= kRefFetch (a
+ * stack entry of it would not carry its count), |= 2 when some leaf does not start at a triangle boundary or reaches
+ * past the draw's derived records (first % 3 != 0 or first + count > lim3 = 3 * triangles: its triangles would need
+ * the index path). */
+__global__ __launch_bounds__(256) void scan_leaf_counts(const wcpt_node* __restrict__ bvh, uint32_t nodes, uint32_t lim3,
+                                                        uint32_t* __restrict__ flags)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < nodes && bvh[i].triangleCount >= kRefFetch) atomicOr(big, 1u);
+    if (i >= nodes) return;
+    const uint32_t first = bvh[i].leftNodeOrTriangleIndex, count = bvh[i].triangleCount;
+    if (count == 0u) return;
+    uint32_t f = count >= kRefFetch ? 1u : 0u;
+    if (first % 3u != 0u || first > lim3 || count > lim3 - first) f |= 2u;
+    if (f) atomicOr(flags, f);
 }
 
 __global__ __launch_bounds__(256) void build_tri_records(const uint32_t* __restrict__ idx, const float* __restrict__ vtx,
@@ -372,12 +380,13 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
     return hipGetLastError();
 }
 
-hipError_t launch_scan_leaf_counts(const void* bvh, uint32_t nodes, uint32_t* big, hipStream_t stream)
+hipError_t launch_scan_leaf_counts(const void* bvh, uint32_t nodes, uint32_t triangles, uint32_t* flags,
+                                   hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(big, 0, sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess || nodes == 0) return e;
     hipLaunchKernelGGL(dev::scan_leaf_counts, dim3((nodes + 255u) / 256u), dim3(256), 0, stream,
-                       static_cast<const wcpt_node*>(bvh), nodes, big);
+                       static_cast<const wcpt_node*>(bvh), nodes, 3u * triangles, flags);
     return hipGetLastError();
 }
 

@@ -116,6 +116,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_SMALL_LEAVES
 #define WCPT_WF_SMALL_LEAVES 1 /* the fast layout also requires kTriFlagSmallLeaves: packed stack entries need no fetch case */
 #endif
+#ifndef WCPT_WF_LEAF_RECORDS
+#define WCPT_WF_LEAF_RECORDS 1 /* the fast layout also requires kTriFlagLeafRecords: leaf steps need no index path */
+#endif
 #ifndef WCPT_WF_GEO2_WAVES
 #define WCPT_WF_GEO2_WAVES 8 /* occupancy floor of the fast-layout trace (waves per SIMD) */
 #endif
@@ -496,8 +499,12 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             if (has && mode == kModeLeaf) {
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
-                const uint32_t off = g.idx24 ? tri_record_off24(ca, g.lim3) : cr;
-                leaf_step(off != kNoRecord ? load_tri_at(g.tris, off) : index_tri());
+                if (GEO == 2 && WCPT_WF_LEAF_RECORDS) {
+                    leaf_step(load_tri_at(g.tris, ca * 16u)); /* every leaf triangle has its record (kTriFlagLeafRecords) */
+                } else {
+                    const uint32_t off = g.idx24 ? tri_record_off24(ca, g.lim3) : cr;
+                    leaf_step(off != kNoRecord ? load_tri_at(g.tris, off) : index_tri());
+                }
             }
             diag_mark<DIAG>(tim, tprev, 1);
             if (has && mode == kModeDone) {

@@ -83,7 +83,9 @@ struct TriRecords {
      * triangleCount < 255 (pt_device.h kTriFlagSmallLeaves) */
     uint64_t bvh = 0, gen_bvh = kUnknownGeneration;
     uint64_t bvh_nodes = 0;
-    bool small_leaves = false, leaves_valid = false;
+    uint32_t bvh_ntri = 0;
+    uint32_t leaf_flags = 0;   /* launch_scan_leaf_counts */
+    bool leaves_valid = false;
     /* primary-ray pair records (pt_device.h TriPairP) for the camera position `porigin` (bit patterns), derived from
      * the pair records of build `pbuild` */
     void* pmem = nullptr;
@@ -337,21 +339,24 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         if (flags & 1u) {
             /* pt_device.h kTriFlagSmallLeaves: scanned on the device once per BVH buffer generation */
             const uint64_t gb = bb->generation;
-            if (!(ctx->tri_cache && t.leaves_valid && t.bvh == dc[d].bvhBuffer && t.gen_bvh == gb && t.bvh_nodes == nodes)) {
+            if (!(ctx->tri_cache && t.leaves_valid && t.bvh == dc[d].bvhBuffer && t.gen_bvh == gb && t.bvh_nodes == nodes &&
+                  t.bvh_ntri == ntri)) {
                 if (!ctx->d_scan) HIP_TRY(ctx, hipMalloc(&ctx->d_scan, sizeof(uint32_t)), "hipMalloc(leaf scan flag)");
                 HIP_TRY(ctx, wcpt::launch_scan_leaf_counts(reinterpret_cast<const void*>(dc[d].bvhBuffer), (uint32_t)nodes,
-                                                           ctx->d_scan, ctx->stream), "scan_leaf_counts");
-                uint32_t big = 1;
-                HIP_TRY(ctx, hipMemcpyAsync(&big, ctx->d_scan, sizeof(big), hipMemcpyDeviceToHost, ctx->stream),
+                                                           ntri, ctx->d_scan, ctx->stream), "scan_leaf_counts");
+                uint32_t lf = 3;
+                HIP_TRY(ctx, hipMemcpyAsync(&lf, ctx->d_scan, sizeof(lf), hipMemcpyDeviceToHost, ctx->stream),
                         "hipMemcpyAsync(leaf scan flag)");
                 HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(leaf scan flag)");
                 t.bvh = dc[d].bvhBuffer;
                 t.gen_bvh = gb;
                 t.bvh_nodes = nodes;
-                t.small_leaves = big == 0;
+                t.bvh_ntri = ntri;
+                t.leaf_flags = lf;
                 t.leaves_valid = true;
             }
-            if (t.small_leaves) flags |= 4u;
+            if (!(t.leaf_flags & 1u)) flags |= 4u; /* pt_device.h kTriFlagSmallLeaves */
+            if (!(t.leaf_flags & 2u)) flags |= 8u; /* pt_device.h kTriFlagLeafRecords */
         }
         flags |= (uint64_t)nvert << 32;                 /* pt_device.h draw_vertex_count: bounds the index path */
         /* word 2: ntri, and in its high half the BVH node count when packed refs apply (the buffer-resource node loads
@@ -369,7 +374,7 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         leaves_all += bb ? (bb->bytes / sizeof(wcpt_node) + 1u) / 2u : ntri; /* unknown BVH: assume thin leaves */
     }
     /* the wavefront trace's one-draw fast layout: packed stack refs, 24-bit record offsets, buffer-resource node loads */
-    a.wf_fast = n == 1 && (ctx->tri_table[3] & 7u) == 7u && (ctx->tri_table[2] >> 32) > 0;
+    a.wf_fast = n == 1 && (ctx->tri_table[3] & 15u) == 15u && (ctx->tri_table[2] >> 32) > 0;
     /* pair leaves address a draw's pair records with 32-bit byte offsets (pt_device.h load_pair_at) */
     a.pair_records = tris_max <= kPairMaxTriangles &&
                      (ctx->pair_records == 1 ||
