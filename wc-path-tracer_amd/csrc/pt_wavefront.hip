@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
  * entries run within 1%, 24 is 13% slower -- the traversal is bound by node-fetch latency, not the spill). */
 constexpr int wf_lds_per_wave(int n) { return n * 512; }
 constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
-enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3 };
+enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3, kModeIdle = 4 };
 
 #ifndef WCPT_WF_TRACE_SHARE
 #define WCPT_WF_TRACE_SHARE 1
@@ -280,7 +280,9 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
         g0.idx24 = true;
     }
 
-    bool has = false, drained = false, tail_claims = false;
+    /* a lane without a ray is in kModeIdle (no separate `has` flag: its lane mask had to be carried through every
+     * divergent block of the loop) */
+    bool drained = false, tail_claims = false;
     /* this wave's claimed queue range [lo, hi) (wave-uniform). The first chunk is static (chunk blockIdx.x), so a
      * launch with fewer rays than resident waves costs no atomics for the waves without work: same-address
      * device-scope atomics serialise, and one per wave of the persistent grid cost ~0.28 ms per launch. Later
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
         drained = true;
     }
     uint32_t p = 0, d = 0, prim = kNoPrim, primDraw = 0;
-    uint32_t ca = 0, cb = 0, cr = 0, mode = kModeDone;
+    uint32_t ca = 0, cb = 0, cr = 0, mode = kModeIdle;
     float rt = kInfinity;
     bool any = false; /* this ray is the last segment of its pixel's last sample (render build only) */
     RefStack rf;      /* the reference's stack index (counting builds, pt_device.h RefStack) */
@@ -323,8 +325,10 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
     for (;;) {
         /* dynamic fetch: idle lanes take the next queued rays, once at least `refill` lanes are idle (or none
          * has work left) */
-        unsigned long long need = __ballot(!has);
-        if (!drained && ((uint32_t)__popcll(need) >= refill || need == ~0ull)) {
+        unsigned long long need = __ballot(mode == kModeIdle);
+        /* refill <= 64 (wcpt_set_option), so "every lane idle" is included in popcount >= refill; all 64 lanes stay in
+         * the loop until the wave leaves it */
+        if (!drained && (uint32_t)__popcll(need) >= refill) {
             while (need) {
                 if (lo == hi) {
                     uint32_t base = 0;
@@ -371,7 +375,6 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                     if (COUNT) simd_step<DIAG>(cnt.wave_seg, cnt.lane_seg);
                     d = 0;
                     start_draw();
-                    has = true;
                 }
                 const uint32_t took = min(avail, (uint32_t)__popcll(need));
                 lo += took;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             }
         }
         if (DIAG && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memtime();
-        if (!__ballot(has)) break;
+        if (!__ballot(mode != kModeIdle)) break;
         diag_mark<DIAG>(tim, tprev, 0);
         {
             const Geom& g = SINGLE ? g0 : gl;
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
              * an interior node fetches its children in the same iteration, and one that descends into a leaf tests
              * its first triangle in the same iteration (measured 1.4% faster than leaf -> interior -> pop). Each
              * lane still executes exactly the reference's sequence of steps. */
-            if (has && mode == kModePop) {
+            if (mode == kModePop) {
 #if WCPT_WF_POP_ONCE
                 /* one stack entry per iteration: a culled entry (:162) leaves the lane in pop mode */
                 if (stk.empty()) {
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 return tri_from_indices(g.indices, g.vertices, ca, draw_vertex_count(tri_records, SINGLE ? 0u : d));
             };
             diag_mark<DIAG>(tim, tprev, 3); /* pop */
-            if (has && mode == kModeInterior) {
+            if (mode == kModeInterior) {
                 NodeV L, R;
                 if (WCPT_WF_PAIR_RSRC && (GEO == 2 || g.nodes)) {
                     load_pair_rsrc(g.rsrc, ca, L, R);
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 interior_step(L, R);
             }
             diag_mark<DIAG>(tim, tprev, 2);
-            if (has && mode == kModeLeaf) {
+            if (mode == kModeLeaf) {
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
                 if (GEO == 2 && WCPT_WF_LEAF_RECORDS) {
@@ -507,11 +510,11 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 }
             }
             diag_mark<DIAG>(tim, tprev, 1);
-            if (has && mode == kModeDone) {
+            if (mode == kModeDone) {
                 /* Intersect result; wf_shade rebuilds the winner's normal and material (:204-208) */
                 b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
                 ref_segment_end<COUNT>(cnt);
-                has = false;
+                mode = kModeIdle;
             }
             diag_mark<DIAG>(tim, tprev, 4);
         }
