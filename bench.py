@@ -287,9 +287,11 @@ def main():
     ap.add_argument("--bvh", default="midpoint", choices=["midpoint", "sah"],
                     help="BVH builder: the reference's midpoint split (default: the benchmarked workload) or the "
                          "optional binned SAH (a different tree, reported as a separate workload)")
-    ap.add_argument("--gather", default="rgb", choices=["rgb", "rgba"],
+    ap.add_argument("--gather", default="rgb", choices=["rgb", "rgba", "display"],
                     help="N>1 wire format of the row blocks: rgb (default; alpha is always 1.0 and is restored on "
-                         "rank 0, bit-identical frame, 12 B/px) or the full rgba32f block (16 B/px)")
+                         "rank 0, bit-identical frame, 12 B/px), the full rgba32f block (16 B/px), or display: "
+                         "composite.comp's RGBA8 display value written by the render itself "
+                         "(WCPT_PAYLOAD_DISPLAY_RGBA8, 4 B/px; what rank 0 presents, not the accumulation)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: gather each frame on the render stream instead of overlapping it with the next render")
     ap.add_argument("--verify", action="store_true",
@@ -362,7 +364,9 @@ def main():
         max_rows = -(-H // world)
         shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
         ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
-        channels = 3 if args.gather == "rgb" else 4
+        # payload format code of wcpt_set_gather_output: 3 / 4 float channels, or 8 = WCPT_PAYLOAD_DISPLAY_RGBA8
+        channels = {"rgb": 3, "rgba": 4, "display": 8}[args.gather]
+        pdt, pch = (torch.uint8, 4) if args.gather == "display" else (torch.float32, channels)
         # The gather payload is written by the render itself (wcpt_set_gather_output): each frame's kernel stores the
         # rank's row block as RGB (alpha is always 1.0 and is restored on rank 0) or RGBA into one of the payload
         # buffers, so no copy kernel runs between the render and the collective. Overlap: frame k's payload is
@@ -373,8 +377,8 @@ def main():
         # render-stream wait on that event.
         nbuf = 3 if overlap else 1
         comm = torch.cuda.Stream(device=device) if overlap else None
-        payload = [torch.empty((max_rows, W, channels), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
-        gathered = [[torch.empty(payload[0].shape, dtype=torch.float32, device="cpu" if host_staged else "cuda")
+        payload = [torch.empty((max_rows, W, pch), dtype=pdt, device="cuda") for _ in range(nbuf)]
+        gathered = [[torch.empty(payload[0].shape, dtype=pdt, device="cpu" if host_staged else "cuda")
                      for _ in range(world)] for _ in range(nbuf)] if rank == 0 else None
         last = {"buf": 0}
         ready_ev = [torch.cuda.Event() for _ in range(nbuf)]   # payload[i] holds frame k's block
@@ -388,7 +392,7 @@ def main():
             out = gathered[i] if rank == 0 else None
             if overlap and done_used[i]:
                 done_ev[i].synchronize()                    # payload[i]'s gather (frame k-3) has finished
-            ctx.set_gather_output(payload[i].data_ptr(), payload[i].numel() * 4, channels)
+            ctx.set_gather_output(payload[i].data_ptr(), payload[i].numel() * payload[i].element_size(), channels)
             ctx.render(sd, *addrs)
             if not overlap:
                 dist.gather(payload[i].cpu() if host_staged else payload[i], out, dst=0)
@@ -475,9 +479,16 @@ def main():
             vctx.create_screen(W, H)
             for f in range(args.warmup + args.steps):
                 vctx.render(scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f), *vdev.addresses())
-            ref = vctx.readback()
+            if world > 1 and args.gather == "display":
+                disp = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+                vctx.composite(disp.data_ptr(), rgba8=True)
+                vctx.sync()
+                ref = disp.cpu().numpy()
+            else:
+                ref = vctx.readback()
             vdev.free()
-        same = frame_img.view(np.uint32) == ref.view(np.uint32)
+        bits = np.uint8 if ref.dtype == np.uint8 else np.uint32  # display bytes, or the float image's bit patterns
+        same = frame_img.view(bits) == ref.view(bits)
         verified = bool(same.all())
         if not verified:
             bad_rows = np.nonzero(~same.all(axis=(1, 2)))[0]

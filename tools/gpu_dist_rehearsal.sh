@@ -17,6 +17,10 @@ for n in 2 3; do
 done
 run n2_c1_rgba 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29520 bench.py --gpus 2 --config c1 --steps 4 --warmup 2 --dist-backend gloo --gather rgba --verify || exit 1
+run n2_c1_display 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29521 bench.py --gpus 2 --config c1 --steps 4 --warmup 2 --dist-backend gloo --gather display --verify || exit 1
+run n3_c2_display_host 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 \
+    --master-port 29522 bench.py --gpus 3 --config c2 --steps 4 --warmup 2 --dist-backend gloo-host --gather display --verify || exit 1
 run n2_c2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29510 bench.py --gpus 2 --config c2 --steps 5 --warmup 2 --dist-backend gloo --verify || exit 1
 run n2_c3 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
