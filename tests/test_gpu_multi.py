@@ -172,3 +172,58 @@ def test_two_ranks_libwcpt_gather_equals_one_device(gpu_ctx, tmp_path, kernel):
     for f in frames:
         acc, _ = oracle.render_scene(s, W, H, max_bounce=4, frame=f, image=acc, threads=8)
     assert_close(got, acc)
+
+
+def _rank_display(rank, world, port, W, H, frames, kernel, out_path):
+    """One rank of the display-payload gather (bench.py --gather display): the render itself writes composite.comp's
+    RGBA8 display value of the rank's row block into a device payload (WCPT_PAYLOAD_DISPLAY_RGBA8), which travels
+    at 4 B/px."""
+    import sys
+    import torch
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "wc-path-tracer_amd")]
+    import wcpt as w
+    from wcpt import scene as wscene
+    from wcpt.dist import assemble, row_block
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = wscene.generate("cornell")
+    y0, rows = row_block(H, world, rank)
+    payload = torch.zeros((-(-H // world), W, 4), dtype=torch.uint8, device="cuda")
+    with w.Context(0) as ctx:
+        dev = w.DeviceScene(ctx, s)
+        ctx.set_kernel(kernel)
+        ctx.create_screen(W, H)
+        ctx.set_row_range(y0, rows)
+        ctx.set_gather_output(payload.data_ptr(), payload.numel(), w._lib.PAYLOAD_DISPLAY_RGBA8)
+        for f in frames:
+            ctx.render(s.scene_data(W, H, max_bounce=4, frame=f), *dev.addresses())
+        ctx.sync()
+        dev.free()
+    block = payload.cpu()
+    parts = [torch.empty_like(block) for _ in range(world)] if rank == 0 else None
+    dist.gather(block, parts, dst=0)
+    if rank == 0:
+        np.save(out_path, assemble(parts, H, world).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_two_ranks_display_payload_gather_equals_oracle_composite(gpu_ctx, tmp_path, kernel):
+    """Two ranks render their row blocks with the RGBA8 display payload written by the render, gather the 4-B/px
+    blocks over gloo, and rank 0's frame equals composite.comp (oracle.composite) of the oracle's accumulated frame
+    byte for byte (composite.comp:36-53)."""
+    W, H, frames = 64, 45, (0, 1, 2)
+    out = str(tmp_path / "display.npy")
+    mp.spawn(_rank_display, args=(2, _free_port(), W, H, frames, kernel, out), nprocs=2, join=True)
+    got = np.load(out)
+    s = get_scene("cornell")
+    acc = None
+    for f in frames:
+        acc, _ = oracle.render_scene(s, W, H, max_bounce=4, frame=f, image=acc, threads=8)
+    _, want = oracle.composite(acc)
+    assert got.dtype == np.uint8 and got.shape == (H, W, 4)
+    assert np.array_equal(got, want)
