@@ -1,18 +1,24 @@
 """bench.py — Mray/s + ms/frame of the MI355X path-tracing compute path (BASELINE.json metric).
 
 Default workload (N=1): BASELINE.json configs[1] = Cornell box (34 triangles + 4 spheres), 1920x1080, 1 spp,
-maxBounceCount 4, progressive frames (renderedFramesCount = 0, 1, 2, ...). A "step" is one frame: one
-wcpt_render over the whole frame (with N ranks: each rank renders its row block, SURVEY.md §8(e), and the
-blocks are gathered to rank 0 over RCCL). Rays = ray segments = Intersect() calls, counted exactly by the
-instrumented kernel for the very frames that were timed (untimed re-run).
+maxBounceCount 4, progressive frames (renderedFramesCount = 0, 1, 2, ...). A "step" is one frame: one render of the
+whole frame (with N ranks: each rank renders its row block, SURVEY.md §8(e), and the blocks are gathered to the root
+over RCCL). Rays = ray segments = Intersect() calls, counted exactly by the instrumented kernel for the very frames
+that were timed (untimed re-run).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|ref] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|ref] [--camera still|orbit]
+                    [--transport rccl|copy] [--devices 0,1,..] [--verify] [--no-cpu-baseline]
 
-Prints one JSON line on rank 0.
-
-N = 1 runs on the product's own runtime: torch is NOT imported, libwcpt.so binds the system HIP runtime (/opt/rocm)
-exactly as the Jai host would, renders on the context's own stream and is timed with host clocks around
-wcpt_sync (the JSON line's "hip_runtime" names the runtime). N > 1 imports torch for torch.distributed (RCCL).
+Prints one JSON line on rank 0. Every mode drives the product's C ABI (include/wcpt.h wcpt_group_*) on the system HIP
+runtime (/opt/rocm), as the Jai host would; torch is not imported:
+  - no WORLD_SIZE (plain `python bench.py --gpus N`): one process, one host thread, a group over devices 0..N-1
+    (wcpt_group_create_ex; RCCL ncclCommInitAll, or --transport copy). --gpus 1 is a group of one, which renders
+    exactly as a single context.
+  - under torchrun (WORLD_SIZE = N): one process per GPU, rank RANK on device LOCAL_RANK (wcpt_group_create_rank,
+    ncclCommInitRank); the 128-byte RCCL id, barriers and the max-over-ranks time go through a TCP rendezvous
+    (wcpt.rdzv, MASTER_ADDR:MASTER_PORT+1). --gpus, if given, must equal WORLD_SIZE.
+  - --dist-backend gloo | gloo-host | torch-nccl under torchrun: the torch.distributed gather of rounds 1-3 (torch
+    imported first, so libwcpt binds torch's bundled HIP runtime): N-rank rehearsals on one GPU.
 """
 from __future__ import annotations
 
@@ -22,19 +28,12 @@ import os
 import sys
 import time
 
-WORLD = int(os.environ.get("WORLD_SIZE", "1"))
-if WORLD > 1:
-    # torch first: libwcpt.so then binds to the HIP runtime torch already loaded (one runtime per process).
-    import torch  # noqa: E402
-    import torch.distributed as dist  # noqa: E402
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "wc-path-tracer_amd")]
 
 import numpy as np  # noqa: E402
-import wcpt  # noqa: E402
-from wcpt import scene as wscene  # noqa: E402
-from wcpt.dist import assemble, row_block  # noqa: E402
+
+wcpt = None  # libwcpt.so's binding, imported in main() once the process knows which HIP runtime it binds
 
 CONFIGS = {
     # name: (scene, width, height, spp, maxBounceCount, description)
@@ -48,18 +47,28 @@ CONFIGS = {
                                                 "maxBounceCount 3"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-BASELINE_METRIC = "Mray/s + ms/frame at 1920\u00d71080 1spp; achieved HBM GB/s vs peak"  # BASELINE.json "metric"
+BASELINE_METRIC = "Mray/s + ms/frame at 1920×1080 1spp; achieved HBM GB/s vs peak"  # BASELINE.json "metric"
 # rays = ray segments (Intersect() calls), counted exactly by the instrumented kernel
-# Measured best kernel per workload: the megakernel wins on the coherent, L1-resident
-# Cornell box; the wavefront variant wins on the 262k-triangle atrium (incoherent, MALL-resident).
-DEFAULT_KERNEL = {"c1": wcpt.KERNEL_MEGAKERNEL, "c2": wcpt.KERNEL_MEGAKERNEL, "c3": wcpt.KERNEL_WAVEFRONT,
-                  "c4": wcpt.KERNEL_WAVEFRONT, "ref": wcpt.KERNEL_MEGAKERNEL}
-# VALU issue ceiling (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 4 cycles at the
-# 2.4 GHz peak engine clock (tools/valu_peak.hip measures it: profiles/r03_valu_peak.log)
+# Measured best kernel per workload: the megakernel (WCPT_KERNEL_MEGAKERNEL = 0) wins on the
+# coherent, L1-resident Cornell box; the wavefront variant (WCPT_KERNEL_WAVEFRONT = 2) on the 262k-triangle atrium.
+KERNEL_MEGAKERNEL, KERNEL_WAVEFRONT = 0, 2
+DEFAULT_KERNEL = {"c1": KERNEL_MEGAKERNEL, "c2": KERNEL_MEGAKERNEL, "c3": KERNEL_WAVEFRONT, "c4": KERNEL_WAVEFRONT,
+                  "ref": KERNEL_MEGAKERNEL}
+# VALU issue ceiling (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs at the 2.4 GHz peak engine clock; a wave64 VALU
+# instruction issues over 2 cycles on the 32-lane SIMD (tools/valu_peak.hip measures the rates: profiles/r03_valu_peak*.log)
 SIMDS = 1024
 CLOCK_GHZ = 2.4
-CYCLES_PER_VALU = 2  # a wave64 VALU instruction issues over 2 cycles on the 32-lane SIMD (MI355X_MICROARCH.md)
+CYCLES_PER_VALU = 2
 VALU_PEAK_GINSTR = SIMDS * CLOCK_GHZ / CYCLES_PER_VALU  # spec: 1,228.8 G wave64 VALU instructions/s
+# the gathered frame's wire format (wcpt.h WCPT_PAYLOAD_*) and its bytes per pixel
+GATHER_FORMATS = {"rgb": (3, 12), "rgba": (4, 16), "display": (8, 4)}
+# --camera orbit: the editor's camera while the user strafes (D / A at 4.0 * deltaTime, editor.jai:91,105-112) and drags
+# with the right mouse button (yaw, editor.jai:138-143), at 60 frames/s, turning back every ORBIT_HALF_PERIOD frames so
+# the camera stays in the scene (0.8 units of travel each way: the Cornell box spans [-1, 1]); every such frame resets
+# renderedFramesCount to 0 (editor.jai:149-150)
+ORBIT_DT = 1.0 / 60.0
+ORBIT_YAW_DEG = 0.5
+ORBIT_HALF_PERIOD = 12
 
 
 def algorithmic_bytes(c: dict) -> int:
@@ -77,7 +86,8 @@ def _profile_json(path, args):
         pm = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if pm.get("config") == args.config and pm.get("kernel") == args.kernel and args.bvh == "midpoint":
+    if (pm.get("config") == args.config and pm.get("kernel") == args.kernel and args.bvh == "midpoint" and
+            getattr(args, "camera", "still") == pm.get("camera", "still")):
         return pm
     return None
 
@@ -92,15 +102,17 @@ def roofline(args, tot, render_s, frame_s) -> dict:
     memory_latency (wavefront trace; c3): dependent scene-line visits (one 64-B child pair per interior visit, one
       triangle record per test) per second of the frame, against the best rate of dependent random line visits the
       cache hierarchy sustains at 8 waves/SIMD (L2-resident chain, tools/gather_bench.hip, profiles/gather_ceiling.json).
-    Beside it: the SURVEY 8(d) algorithmic bytes, which price every scene fetch at HBM cost although these scenes are
-      served from L1/L2/MALL (so they exceed the HBM peak: "cache-served"), and the HBM bytes the PMC counters measured
-      (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction), the only true HBM load."""
+    Beside it: the HBM bytes the PMC counters measured (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction), the only
+      true HBM load, and under not_a_roofline the SURVEY 8(d) algorithmic bytes, which price every scene fetch at HBM
+      cost although these scenes are served from L1/L2/MALL."""
     steps = max(1, args.steps)
     alg_bytes = algorithmic_bytes(tot) / steps
-    r = {"algorithmic_bytes_per_render": int(alg_bytes),
-         "algorithmic_gbs": round(alg_bytes / render_s / 1e9, 1),
-         "algorithmic_frac": round(alg_bytes / render_s / 1e9 / HBM_PEAK_GBS, 3),
-         "algorithmic_note": "cache-served: SURVEY 8(d) bytes priced at HBM cost; the scene stays in L1/L2/MALL"}
+    # SURVEY 8(d)'s bytes price every scene fetch at HBM cost, but these scenes are served from L1/L2/MALL, so their
+    # rate exceeds the HBM peak: kept for reference, outside the roofline head (every frac there is physical, <= 1)
+    r = {"not_a_roofline": {"algorithmic_bytes_per_render": int(alg_bytes),
+                            "algorithmic_gbs": round(alg_bytes / render_s / 1e9, 1),
+                            "note": "cache-served: SURVEY 8(d) bytes priced at HBM cost; the scene stays in "
+                                    "L1/L2/MALL, so this is not an HBM rate"}}
     pm = _profile_json(args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json"), args)
     traffic = None if pm is None else pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_frame"))
     r["traffic"] = traffic
@@ -265,9 +277,12 @@ def cpu_baseline(scene, width, height, spp, bounces, budget_s=20.0, min_frames=5
                       f"{t_total:.1f} s on {where}"}
 
 
-def main():
+
+# ---- topology and frame sequence (host logic, CPU-tested: tests/test_bench_cli.py) ------------------------------------
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default 1; under torchrun WORLD_SIZE, which --gpus must then equal)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--settle-ms", type=float, default=200.0,
@@ -279,6 +294,10 @@ def main():
                     help="0 megakernel, 2 wavefront, -1 per-config default (DEFAULT_KERNEL)")
     ap.add_argument("--wf-pipes", type=int, default=0,
                     help="wavefront kernel: concurrent pipelines (WCPT_OPTION_WF_PIPES; 0 = the library default)")
+    ap.add_argument("--camera", default="still", choices=["still", "orbit"],
+                    help="still: progressive frames of a still camera (renderedFramesCount = 0, 1, ...); orbit: the "
+                         "camera moves every frame as in an editor drag (strafe + yaw, renderedFramesCount = 0 each "
+                         "frame, editor.jai:149-150), so the primary-ray records are rebuilt for every frame")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--pmc-json", default=None,
@@ -287,226 +306,466 @@ def main():
     ap.add_argument("--bvh", default="midpoint", choices=["midpoint", "sah"],
                     help="BVH builder: the reference's midpoint split (default: the benchmarked workload) or the "
                          "optional binned SAH (a different tree, reported as a separate workload)")
-    ap.add_argument("--gather", default="rgb", choices=["rgb", "rgba", "display"],
+    ap.add_argument("--gather", default="rgb", choices=sorted(GATHER_FORMATS),
                     help="N>1 wire format of the row blocks: rgb (default; alpha is always 1.0 and is restored on "
-                         "rank 0, bit-identical frame, 12 B/px), the full rgba32f block (16 B/px), or display: "
+                         "the root, bit-identical frame, 12 B/px), the full rgba32f block (16 B/px), or display: "
                          "composite.comp's RGBA8 display value written by the render itself "
-                         "(WCPT_PAYLOAD_DISPLAY_RGBA8, 4 B/px; what rank 0 presents, not the accumulation)")
+                         "(WCPT_PAYLOAD_DISPLAY_RGBA8, 4 B/px; what the root presents, not the accumulation)")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="N>1: gather each frame on the render stream instead of overlapping it with the next render")
+                    help="N>1: gather each frame in line with the renders instead of overlapping it with the next "
+                         "render (WCPT_GROUP_OPTION_OVERLAP 0)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "copy"],
+                    help="one-process group: RCCL send/recv (default) or hipMemcpyPeerAsync of each block")
+    ap.add_argument("--devices", default=None,
+                    help="one-process group: device of each rank, comma-separated (default 0..N-1); a device listed "
+                         "more than once rehearses N ranks on fewer GPUs (needs --transport copy)")
     ap.add_argument("--verify", action="store_true",
-                    help="rank 0 re-renders the timed frame sequence on the full frame and checks the gathered "
-                         "row blocks against it bit-for-bit (adds 'verified' to the JSON line)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo", "gloo-host"],
-                    help="nccl (= RCCL over xGMI, the product path); gloo (device tensors) or gloo-host (host-staged) "
-                         "rehearse N>1 ranks on one GPU, where RCCL refuses duplicate devices")
-    args = ap.parse_args()
+                    help="the root re-renders the timed frame sequence on one device and checks the presented frame "
+                         "against it bit for bit (adds 'verified' to the JSON line)")
+    ap.add_argument("--dist-backend", default="rccl", choices=["rccl", "gloo", "gloo-host", "torch-nccl"],
+                    help="under torchrun: rccl (default) = the product's one-process-per-device group over RCCL, no "
+                         "torch; gloo / gloo-host / torch-nccl = the torch.distributed gather (gloo rehearses N ranks "
+                         "on one GPU, where RCCL refuses two ranks on one device)")
+    return ap.parse_args(argv)
 
 
-    world = WORLD
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    name, W, H, spp, bounces, desc = CONFIGS[args.config]
-    if args.kernel < 0:
-        args.kernel = DEFAULT_KERNEL[args.config]
-    scene = wscene.generate(name, bvh=args.bvh)
-    y0, rows = row_block(H, world, rank)
-    overlap = world > 1 and not args.no_overlap
-    host_staged = world > 1 and args.dist_backend == "gloo-host"
-    # Per-step host work is kept small (at 8 ranks a c2 row block renders in ~0.1 ms): the camera is static, so
-    # SceneData is built once and only renderedFramesCount changes per frame (PathTracingRenderer.jai:423).
-    sd = scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=0)
+def resolve_topology(args, env) -> dict:
+    """Which ranks this process drives. Raises SystemExit on a contradiction instead of measuring something else."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world > 1:
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}: one rank per "
+                             f"GPU, so they must agree")
+        if args.devices:
+            raise SystemExit("bench.py: --devices is for the one-process group (no WORLD_SIZE)")
+        local = int(env.get("LOCAL_RANK", env.get("RANK", "0")))
+        return {"mode": "ranks" if args.dist_backend == "rccl" else "torch", "nranks": world,
+                "rank": int(env.get("RANK", "0")), "local_rank": local, "devices": [local]}
+    if args.dist_backend != "rccl":
+        raise SystemExit(f"bench.py: --dist-backend {args.dist_backend} needs a torchrun launch (WORLD_SIZE > 1)")
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}")
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
+    if len(devices) != n:
+        raise SystemExit(f"bench.py: --devices names {len(devices)} devices for --gpus {n}")
+    if len(set(devices)) < n and args.transport != "copy":
+        raise SystemExit("bench.py: a device listed twice needs --transport copy (RCCL: one rank per device)")
+    return {"mode": "group", "nranks": n, "rank": 0, "local_rank": 0, "devices": devices}
 
-    if world == 1:
-        # The product's runtime: no torch in the process, so libwcpt.so binds /opt/rocm's HIP runtime as a Jai host
-        # would; the context renders on its own stream into its own image (wcpt_create_screen), timed by host clocks
-        # around wcpt_sync (which waits for that stream).
-        device = local % max(1, wcpt.device_count())
-        ctx = wcpt.Context(device)
-        ctx.set_kernel(args.kernel)
-        if args.wf_pipes:
-            ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
-        dev = wcpt.DeviceScene(ctx, scene)
-        ctx.create_screen(W, H)
-        addrs = dev.addresses()
 
-        def step(frame):
-            sd["renderedFramesCount"] = frame
-            ctx.render(sd, *addrs)
+def orbit_camera(cam, step: int):
+    """The editor's camera after `step` frames of strafing while dragging (editor.jai:88-143): D with a rightward drag
+    for ORBIT_HALF_PERIOD frames, then A with a leftward drag as long, and so on, applied from `cam`."""
+    c = type(cam)()
+    import ctypes as C
+    C.pointer(c)[0] = cam
+    for i in range(step):
+        sign = 1.0 if (i // ORBIT_HALF_PERIOD) % 2 == 0 else -1.0
+        yaw90 = np.radians(c.yaw + 90.0)
+        speed = 4.0 * ORBIT_DT
+        c.position[0] += sign * float(np.cos(yaw90)) * speed
+        c.position[2] += sign * float(np.sin(yaw90)) * speed
+        c.yaw -= sign * ORBIT_YAW_DEG
+    return c
 
-        def sync():
-            ctx.sync()
 
-        def barrier():
-            pass
-    else:
-        device = local % max(1, torch.cuda.device_count())  # == local on a node with >= N GPUs
+class FrameSource:
+    """SceneData of frame k of the run (settle frames use k = 0). Still camera: renderedFramesCount = k (progressive
+    accumulation). Orbit: camera moved k editor steps, renderedFramesCount = 0 (editor.jai:149-150). The SceneData
+    arrays are built before the timed region (host camera math is not the path)."""
+
+    def __init__(self, scene, W, H, bounces, spp, camera: str, frames: int):
+        self.still = camera == "still"
+        self.sd = [scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=0)]
+        if not self.still:
+            cam = scene.camera
+            self.sd = [scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=0, camera=orbit_camera(cam, k))
+                       for k in range(frames)]
+
+    def __call__(self, k: int):
+        if self.still:
+            sd = self.sd[0]
+            sd["renderedFramesCount"] = k
+            return sd
+        return self.sd[k]
+
+    def copy(self, k: int):
+        return np.array(self(k), copy=True)
+
+
+# ---- drivers: the product's C-ABI group, or the torch.distributed rehearsal ------------------------------------------
+class GroupBench:
+    """wcpt_group_* (include/wcpt.h): all ranks in this process (mode "group") or this process's rank of a
+    one-process-per-device group (mode "ranks", RCCL id through the rendezvous)."""
+
+    def __init__(self, args, topo, scene, W, H, rdzv=None):
+        T = wcpt._lib
+        self.topo, self.W, self.H = topo, W, H
+        if topo["mode"] == "group":
+            transport = T.GROUP_TRANSPORT_COPY if args.transport == "copy" else T.GROUP_TRANSPORT_RCCL
+            self.g = wcpt.Group(topo["devices"], root=0, transport=transport)
+        else:
+            uid = wcpt.group_unique_id() if topo["rank"] == 0 else None
+            uid = rdzv.broadcast(uid)
+            self.g = wcpt.Group.rank(topo["local_rank"], topo["nranks"], topo["rank"], root=0, uid=uid)
+        self.ctxs = self.g.contexts
+        self.ranks = self.g.ranks
+        self.devs = []
+        for c in self.ctxs:
+            c.set_kernel(args.kernel)
+            if args.wf_pipes:
+                c.set_option(T.OPTION_WF_PIPES, args.wf_pipes)
+            self.devs.append(wcpt.DeviceScene(c, scene))
+        self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
+        self.g.create_screen(W, H)
+        self.fmt, self.px = GATHER_FORMATS[args.gather]
+        self.out = None
+        if topo["nranks"] > 1:
+            root = self.g.context(0)
+            nbytes = W * H * self.px
+            if root is not None:
+                self.out = root.buffer_alloc(nbytes)
+                self.g.set_output(self.fmt, root.buffer_address(self.out), nbytes)
+            else:
+                self.g.set_output(self.fmt, 0, 0)
+        self.addr = [list(a) for a in zip(*[d.addresses() for d in self.devs])]
+
+    def render(self, sd):
+        self.g.render(sd, *self.addr)
+
+    def sync(self):
+        self.g.sync()
+
+    def presenting(self, on: bool):
+        if self.topo["nranks"] == 1:
+            return
+        if on:
+            root = self.g.context(0)
+            if root is not None:
+                self.g.set_output(self.fmt, root.buffer_address(self.out), self.W * self.H * self.px)
+            else:
+                self.g.set_output(self.fmt, 0, 0)
+        else:
+            self.g.set_output(0, 0, 0)
+
+    def profile_begin(self):
+        for c in self.ctxs:
+            c.profile_begin()
+
+    def profile_end(self):
+        return [c.profile_end() for c in self.ctxs]
+
+    def counters(self, sd):
+        tot = {}
+        for c, d in zip(self.ctxs, self.devs):
+            for k, v in c.render_counters(sd, *d.addresses()).items():
+                tot[k] = max(tot.get(k, 0), v) if k == "ref_stack_max" else tot.get(k, 0) + v
+        return tot
+
+    def frame(self):
+        """The presented frame on the root's process (None elsewhere): [H, W, 4] float32 (rgb: alpha restored), or
+        [H, W, 4] uint8 for the display format."""
+        root = self.g.context(0)
+        if root is None:
+            return None
+        if self.out is None:
+            return root.readback(self.H)
+        raw = root.buffer_download(self.out, self.W * self.H * self.px)
+        if self.fmt == wcpt._lib.PAYLOAD_DISPLAY_RGBA8:
+            return np.frombuffer(raw, np.uint8).reshape(self.H, self.W, 4)
+        img = np.frombuffer(raw, np.float32).reshape(self.H, self.W, self.fmt)
+        if self.fmt == 3:
+            img = np.concatenate([img, np.ones(img.shape[:2] + (1,), np.float32)], axis=2)
+        return img
+
+    def info(self):
+        return self.g.info()
+
+    def close(self):
+        for d in self.devs:
+            d.free()
+        if self.out is not None:
+            self.g.context(0).buffer_free(self.out)
+        self.g.close()
+
+
+class TorchBench:
+    """The rounds 1-3 multi-process path: each process renders its row block with its own context on device
+    LOCAL_RANK and torch.distributed gathers the render-written payloads on a communication stream (gloo rehearses
+    N ranks on one GPU; torch-nccl is RCCL through torch). torch was imported before libwcpt, so both share torch's
+    bundled HIP runtime."""
+
+    def __init__(self, args, topo, scene, W, H):
+        import torch
+        import torch.distributed as dist
+        from wcpt.dist import row_block
+        self.torch, self.dist = torch, dist
+        self.W, self.H, self.world, self.rank = W, H, topo["nranks"], topo["rank"]
+        device = topo["local_rank"] % max(1, torch.cuda.device_count())
         torch.cuda.set_device(device)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dist_backend == "nccl":
+        if args.dist_backend == "torch-nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
-        # One explicit stream for everything: the renders (wcpt), the payload hand-off and the collective. Torch's
-        # default current stream is the legacy null stream (handle 0), which wcpt_set_stream takes as "use the
-        # context's own stream" -- that would leave the gather unordered with the render.
-        stream = torch.cuda.Stream(device=device)
-        torch.cuda.set_stream(stream)
-        ctx = wcpt.Context(device)
-        ctx.set_stream(stream.cuda_stream)
-        ctx.set_kernel(args.kernel)
+        self.host_staged = args.dist_backend == "gloo-host"
+        # one explicit stream for the renders and the payload hand-off (torch's default stream handle 0 would be read
+        # by wcpt_set_stream as "the context's own stream", leaving the gather unordered with the render)
+        self.stream = torch.cuda.Stream(device=device)
+        torch.cuda.set_stream(self.stream)
+        self.ctx = wcpt.Context(device)
+        self.ctx.set_stream(self.stream.cuda_stream)
+        self.ctx.set_kernel(args.kernel)
         if args.wf_pipes:
-            ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
-        dev = wcpt.DeviceScene(ctx, scene)
-        ctx.create_screen(W, H)
-        ctx.set_row_range(y0, rows)
-        addrs = dev.addresses()
-        max_rows = -(-H // world)
-        shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
-        ctx.set_external_image(shard.data_ptr(), shard.numel() * 4)
-        # payload format code of wcpt_set_gather_output: 3 / 4 float channels, or 8 = WCPT_PAYLOAD_DISPLAY_RGBA8
-        channels = {"rgb": 3, "rgba": 4, "display": 8}[args.gather]
-        pdt, pch = (torch.uint8, 4) if args.gather == "display" else (torch.float32, channels)
-        # The gather payload is written by the render itself (wcpt_set_gather_output): each frame's kernel stores the
-        # rank's row block as RGB (alpha is always 1.0 and is restored on rank 0) or RGBA into one of the payload
-        # buffers, so no copy kernel runs between the render and the collective. Overlap: frame k's payload is
-        # gathered on a separate communication stream while frame k+1 renders into another buffer. Every frame is
-        # still rendered and gathered; the timed region ends with a device-wide synchronize that includes the last
-        # gather. Three payload buffers, and the host (which runs frames ahead of the GPU) waits for a buffer's
-        # previous gather before the render that rewrites it: measured ~6 us/frame cheaper at 8 ranks than a
-        # render-stream wait on that event.
-        nbuf = 3 if overlap else 1
-        comm = torch.cuda.Stream(device=device) if overlap else None
-        payload = [torch.empty((max_rows, W, pch), dtype=pdt, device="cuda") for _ in range(nbuf)]
-        gathered = [[torch.empty(payload[0].shape, dtype=pdt, device="cpu" if host_staged else "cuda")
-                     for _ in range(world)] for _ in range(nbuf)] if rank == 0 else None
-        last = {"buf": 0}
-        ready_ev = [torch.cuda.Event() for _ in range(nbuf)]   # payload[i] holds frame k's block
-        done_ev = [torch.cuda.Event() for _ in range(nbuf)]    # the gather that last read payload[i] has finished
-        done_used = [False] * nbuf
+            self.ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
+        self.dev = wcpt.DeviceScene(self.ctx, scene)
+        self.ctx.create_screen(W, H)
+        y0, rows = row_block(H, self.world, self.rank)
+        self.ctx.set_row_range(y0, rows)
+        max_rows = -(-H // self.world)
+        self.shard = torch.zeros((max_rows, W, 4), dtype=torch.float32, device="cuda")
+        self.ctx.set_external_image(self.shard.data_ptr(), self.shard.numel() * 4)
+        self.channels = GATHER_FORMATS[args.gather][0]
+        pdt, pch = (torch.uint8, 4) if args.gather == "display" else (torch.float32, self.channels)
+        self.overlap = not args.no_overlap
+        nbuf = 3 if self.overlap else 1
+        self.comm = torch.cuda.Stream(device=device) if self.overlap else None
+        self.payload = [torch.empty((max_rows, W, pch), dtype=pdt, device="cuda") for _ in range(nbuf)]
+        self.gathered = [[torch.empty(self.payload[0].shape, dtype=pdt, device="cpu" if self.host_staged else "cuda")
+                          for _ in range(self.world)] for _ in range(nbuf)] if self.rank == 0 else None
+        self.ready_ev = [torch.cuda.Event() for _ in range(nbuf)]
+        self.done_ev = [torch.cuda.Event() for _ in range(nbuf)]
+        self.done_used = [False] * nbuf
+        self.k = 0
+        self.last = 0
+        self.on = True
+        self.ctxs = [self.ctx]
+        self.ranks = [self.rank]
 
-        def step(frame):
-            sd["renderedFramesCount"] = frame
-            i = frame % nbuf
-            last["buf"] = i
-            out = gathered[i] if rank == 0 else None
-            if overlap and done_used[i]:
-                done_ev[i].synchronize()                    # payload[i]'s gather (frame k-3) has finished
-            ctx.set_gather_output(payload[i].data_ptr(), payload[i].numel() * payload[i].element_size(), channels)
-            ctx.render(sd, *addrs)
-            if not overlap:
-                dist.gather(payload[i].cpu() if host_staged else payload[i], out, dst=0)
-                return
-            ready_ev[i].record(stream)
-            with torch.cuda.stream(comm):
-                comm.wait_event(ready_ev[i])
-                dist.gather(payload[i].cpu() if host_staged else payload[i], out, dst=0)
-                done_ev[i].record(comm)
-            done_used[i] = True
+    def render(self, sd):
+        if not self.on:
+            self.ctx.render(sd, *self.dev.addresses())
+            return
+        nbuf = len(self.payload)
+        i = self.k % nbuf
+        self.k += 1
+        self.last = i
+        out = self.gathered[i] if self.rank == 0 else None
+        if self.overlap and self.done_used[i]:
+            self.done_ev[i].synchronize()
+        p = self.payload[i]
+        self.ctx.set_gather_output(p.data_ptr(), p.numel() * p.element_size(), self.channels)
+        self.ctx.render(sd, *self.dev.addresses())
+        src = p.cpu() if self.host_staged else p
+        if not self.overlap:
+            self.dist.gather(src, out, dst=0)
+            return
+        self.ready_ev[i].record(self.stream)
+        with self.torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.ready_ev[i])
+            self.dist.gather(p.cpu() if self.host_staged else p, out, dst=0)
+            self.done_ev[i].record(self.comm)
+        self.done_used[i] = True
 
-        def sync():
-            torch.cuda.synchronize()
+    def sync(self):
+        self.torch.cuda.synchronize()
 
-        def barrier():
-            dist.barrier()
+    def presenting(self, on: bool):
+        self.on = on
+        if not on:
+            self.ctx.set_gather_output(0, 0)
+
+    def profile_begin(self):
+        self.ctx.profile_begin()
+
+    def profile_end(self):
+        return [self.ctx.profile_end()]
+
+    def counters(self, sd):
+        return self.ctx.render_counters(sd, *self.dev.addresses())
+
+    def frame(self):
+        if self.rank != 0:
+            return None
+        from wcpt.dist import assemble
+        img = assemble([g.to("cpu") for g in self.gathered[self.last]], self.H, self.world).numpy()
+        return img
+
+    def info(self):
+        return {"nranks": self.world, "local_ranks": 1, "first_local_rank": self.rank, "root": 0, "transport": -1,
+                "overlap": int(self.overlap), "distinct_devices": 1, "broken": 0, "frames": self.k}
+
+    def close(self):
+        self.ctx.set_gather_output(0, 0)
+        self.ctx.set_external_image(0, 0)
+        self.dev.free()
+        self.ctx.close()
+        self.dist.destroy_process_group()
+
+
+class _Collective:
+    """Barriers and the cross-rank sums / maxima of the report, over whichever host channel the mode has."""
+
+    def __init__(self, topo, rdzv=None, torch_dist=None):
+        self.topo, self.rdzv, self.td = topo, rdzv, torch_dist
+
+    def barrier(self):
+        if self.rdzv is not None:
+            self.rdzv.barrier()
+        elif self.td is not None:
+            self.td.barrier()
+
+    def gather_obj(self, obj):
+        """Every rank's obj on rank 0 (list in rank order), None elsewhere."""
+        if self.rdzv is not None:
+            return self.rdzv.gather_obj(obj)
+        if self.td is not None:
+            out = [None] * self.topo["nranks"] if self.topo["rank"] == 0 else None
+            self.td.gather_object(obj, out, dst=0)
+            return out
+        return [obj]
+
+
+def verify_frame(args, topo, scene, W, H, spp, bounces, frames: FrameSource, nframes, got):
+    """The presented frame against one context on the root's device rendering the same frame sequence: bit-equal
+    float bit patterns (rgb: alpha restored), or bytes for the display format (wcpt_composite of that render)."""
+    with wcpt.Context(topo["devices"][0]) as vctx:
+        vdev = wcpt.DeviceScene(vctx, scene)
+        vctx.set_kernel(args.kernel)
+        vctx.create_screen(W, H)
+        for f in range(nframes):
+            vctx.render(frames(f), *vdev.addresses())
+        if got.dtype == np.uint8:
+            buf = vctx.buffer_alloc(W * H * 4)
+            vctx.composite(vctx.buffer_address(buf), rgba8=True)
+            vctx.sync()
+            ref = np.frombuffer(vctx.buffer_download(buf, W * H * 4), np.uint8).reshape(H, W, 4)
+            vctx.buffer_free(buf)
+        else:
+            ref = vctx.readback()
+        vdev.free()
+    bits = np.uint8 if ref.dtype == np.uint8 else np.uint32
+    same = got.view(bits) == ref.view(bits)
+    ok = bool(same.all())
+    if not ok:
+        bad_rows = np.nonzero(~same.all(axis=(1, 2)))[0]
+        print(f"verify: {bad_rows.size} of {H} rows differ (first {bad_rows[:8].tolist()}, last "
+              f"{bad_rows[-4:].tolist()}); pixel fraction {1.0 - same.all(axis=2).mean():.4f}", file=sys.stderr,
+              flush=True)
+        if os.environ.get("WCPT_VERIFY_DUMP"):
+            np.savez(os.environ["WCPT_VERIFY_DUMP"], got=got, ref=ref)
+    return ok
+
+
+def main(argv=None):
+    global wcpt
+    args = parse_args(argv)
+    topo = resolve_topology(args, os.environ)
+    if topo["mode"] == "torch":
+        import torch  # noqa: F401  (first: libwcpt.so then binds the HIP runtime torch loaded; one runtime per process)
+        import torch.distributed as tdist
+    import wcpt as _wcpt
+    wcpt = _wcpt
+    from wcpt import scene as wscene
+    if topo["mode"] != "torch":
+        assert "torch" not in sys.modules, "the C-ABI bench must not load torch's HIP runtime"
+
+    name, W, H, spp, bounces, desc = CONFIGS[args.config]
+    if args.kernel < 0:
+        args.kernel = DEFAULT_KERNEL[args.config]
+    rank, nranks = topo["rank"], topo["nranks"]
+    scene = wscene.generate(name, bvh=args.bvh)
+    frames = FrameSource(scene, W, H, bounces, spp, args.camera, args.warmup + args.steps)
+    rdzv = None
+    if topo["mode"] == "ranks":
+        from wcpt.rdzv import Rendezvous
+        rdzv = Rendezvous.from_env()
+    if topo["mode"] == "torch":
+        drv = TorchBench(args, topo, scene, W, H)
+        coll = _Collective(topo, torch_dist=tdist)
+    else:
+        drv = GroupBench(args, topo, scene, W, H, rdzv)
+        coll = _Collective(topo, rdzv=rdzv)
 
     t_settle = time.perf_counter()
     while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-        sd["renderedFramesCount"] = 0
         for _ in range(8):
-            ctx.render(sd, *addrs)
-        sync()
+            drv.render(frames(0))
+        drv.sync()
     for f in range(args.warmup):
-        step(f)
-    sync()
-    barrier()
-    sync()
-    # Kernel time for the roofline: HIP events around every launch on the render stream. At N = 1 they run inside
-    # the timed region (~1 % of a c2 frame). At N > 1 they are left out of it -- with the gather hand-off they cost
-    # ~16 us of a ~84 us 135-row step (tools/host_step_probe.py --profile) -- and the same frames are re-rendered
-    # afterwards, untimed, with the events on.
-    live_events = world == 1
+        drv.render(frames(f))
+    drv.sync()
+    coll.barrier()
+    drv.sync()
+    # Kernel time for the roofline: HIP events around every render on each rank's render stream. With one rank they
+    # run inside the timed region (~1 % of a c2 frame). With more they are left out of it (at 8 ranks a c2 block
+    # renders in ~0.07 ms, and two event records per render and rank are host work of that order), and the same frames
+    # are re-rendered afterwards, untimed, with the events on and presenting off.
+    live_events = nranks == 1
     if live_events:
-        ctx.profile_begin()
+        drv.profile_begin()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k)
-    sync()
-    barrier()
-    sync()
+        drv.render(frames(args.warmup + k))
+    drv.sync()
     elapsed = time.perf_counter() - t0
+    coll.barrier()
+    got = drv.frame() if args.verify else None
     if not live_events:
-        ctx.set_gather_output(0, 0)
-        ctx.profile_begin()
+        drv.presenting(False)
+        drv.profile_begin()
         for k in range(args.steps):
-            sd["renderedFramesCount"] = args.warmup + k
-            ctx.render(sd, *addrs)
-    kernel_ms, launches = ctx.profile_end()
-    ctx.sync()  # surfaces a traversal-stack overflow, if any
+            drv.render(frames(args.warmup + k))
+    prof = drv.profile_end()
+    drv.sync()  # surfaces a traversal-stack overflow, if any
 
-    # exact work of the timed frames (instrumented kernel, untimed)
-    tot = {k: 0 for k in wcpt.COUNTER_FIELDS}
+    # exact work of the timed frames (instrumented kernel, untimed), this process's ranks
+    tot = {}
     for k in range(args.steps):
-        sdk = scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=args.warmup + k)
-        c = ctx.render_counters(sdk, *addrs)
-        for n in tot:
-            tot[n] = max(tot[n], c[n]) if n == "ref_stack_max" else tot[n] + c[n]
+        for n, v in drv.counters(frames.copy(args.warmup + k)).items():
+            tot[n] = max(tot.get(n, 0), v) if n == "ref_stack_max" else tot.get(n, 0) + v
     if spp > 1:
         # primary segments (samples = 1, no bounce): the same rays every sample of a frame traces first; the render
         # traces them once per pixel and samples 1..spp-1 reuse that record (pt_wavefront.hip wf_shade, pt_device.h)
-        cp = ctx.render_counters(scene.scene_data(W, H, max_bounce=0, samples=1, frame=args.warmup), *addrs)
+        sd0 = frames.copy(args.warmup)
+        sd0["maxBounceCount"], sd0["samples"] = 0, 1
+        cp = drv.counters(sd0)
         tot["reused_primary_lines"] = (spp - 1) * (cp["interior_visits"] + cp["triangle_tests"]) * args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, float(tot["segments"]), float(tot["pixels"] * spp)], dtype=torch.float64,
-                         device="cpu" if host_staged else "cuda")
-        tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t[1:].clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed_max, segs_all, prim_all = float(tmax[0]), float(tsum[0]), float(tsum[1])
-    else:
-        elapsed_max, segs_all, prim_all = elapsed, float(tot["segments"]), float(tot["pixels"] * spp)
+        tot["reused_primary_segments"] = (spp - 1) * cp["segments"] * args.steps
+    per_rank = [{"rank": int(r), "block_ms": round(ms / max(1, n), 4), "launches": int(n)}
+                for r, (ms, n) in zip(drv.ranks, prof)]
+    mine = {"elapsed": elapsed, "tot": tot, "per_rank": per_rank,
+            "kernel_ms": sum(ms for ms, _ in prof), "launches": sum(n for _, n in prof)}
+    allr = coll.gather_obj(json.loads(json.dumps(mine, default=int)))
 
     verified = None
-    if args.verify and rank == 0:
-        if world > 1:
-            frame_img = assemble([g.to("cpu") for g in gathered[last["buf"]]], H, world).numpy()
-        else:
-            frame_img = ctx.readback(H)
-        with wcpt.Context(device) as vctx:
-            vdev = wcpt.DeviceScene(vctx, scene)
-            vctx.set_kernel(args.kernel)
-            vctx.create_screen(W, H)
-            for f in range(args.warmup + args.steps):
-                vctx.render(scene.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f), *vdev.addresses())
-            if world > 1 and args.gather == "display":
-                disp = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
-                vctx.composite(disp.data_ptr(), rgba8=True)
-                vctx.sync()
-                ref = disp.cpu().numpy()
-            else:
-                ref = vctx.readback()
-            vdev.free()
-        bits = np.uint8 if ref.dtype == np.uint8 else np.uint32  # display bytes, or the float image's bit patterns
-        same = frame_img.view(bits) == ref.view(bits)
-        verified = bool(same.all())
-        if not verified:
-            bad_rows = np.nonzero(~same.all(axis=(1, 2)))[0]
-            print(f"verify: {bad_rows.size} of {H} rows differ (first {bad_rows[:8].tolist()}, "
-                  f"last {bad_rows[-4:].tolist()}); pixel fraction {1.0 - same.all(axis=2).mean():.4f}",
-                  file=sys.stderr, flush=True)
-            if os.environ.get("WCPT_VERIFY_DUMP"):
-                np.savez(os.environ["WCPT_VERIFY_DUMP"], got=frame_img, ref=ref)
+    if args.verify and got is not None:
+        verified = verify_frame(args, topo, scene, W, H, spp, bounces, frames, args.warmup + args.steps, got)
 
     if rank == 0:
+        elapsed_max = max(a["elapsed"] for a in allr)
+        T = {}
+        for a in allr:
+            for n, v in a["tot"].items():
+                T[n] = max(T.get(n, 0), v) if n == "ref_stack_max" else T.get(n, 0) + v
+        blocks = sorted((b for a in allr for b in a["per_rank"]), key=lambda b: b["rank"])
+        # the roofline's kernel time: the slowest rank's average render (with one rank, the render itself)
+        avg_kernel_s = max(b["block_ms"] for b in blocks) / 1e3
         ms_per_step = elapsed_max / args.steps * 1e3
+        segs_all, prim_all = float(T["segments"]), float(T["pixels"] * spp)
         value = segs_all / elapsed_max / 1e6
-        avg_kernel_s = kernel_ms / max(1, launches) / 1e3
+        info = drv.info()
+        distinct = info["distinct_devices"] if topo["mode"] == "group" else nranks
+        kind = {"group": "one process, one host thread, all ranks (wcpt_group_create_ex)",
+                "ranks": "one process per GPU (wcpt_group_create_rank, ncclCommInitRank; host rendezvous wcpt.rdzv)",
+                "torch": f"one process per GPU, torch.distributed {args.dist_backend} gather (rehearsal path)"}
+        transport = ("rccl" if info["transport"] == 0 else "copy" if info["transport"] == 1 else args.dist_backend)
         out = {
             "metric": BASELINE_METRIC,
             "value": round(value, 3),
             "unit": "Mray/s",
-            "n_gpus": world,
+            "n_gpus": distinct,
             "steps": args.steps,
             "warmup": args.warmup,
             "settle_ms": args.settle_ms,
@@ -518,45 +777,60 @@ def main():
             "data": "synthetic (procedural scene generated in-process, no dataset)" if name not in
                     wscene.REFERENCE_SCENES else "the reference's own Init scene (mushroom.obj fixture + 4 spheres)",
             "config": {"workload": desc, "config": args.config, "scene": name, "width": W, "height": H,
-                       "spp": spp, "max_bounce": bounces, "frames": "progressive, renderedFramesCount=warmup..",
+                       "spp": spp, "max_bounce": bounces,
+                       "frames": ("progressive, renderedFramesCount=warmup.." if args.camera == "still" else
+                                  "moving camera (editor strafe + yaw every frame), renderedFramesCount=0"),
+                       "camera": args.camera,
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel], "bvh": args.bvh,
-                       "parallelism": f"row-block x{world}" + ((" + RCCL gather" if args.dist_backend == "nccl"
-                                                               else f" + {args.dist_backend} gather (rehearsal)")
-                                                              + f" of {args.gather} blocks"
-                                                              + (" overlapped with the next frame" if overlap else "")
-                                                              if world > 1 else "")},
-            "hip_runtime": hip_runtime_label(world),
+                       "parallelism": (f"row-block x{nranks} + {transport} gather of {args.gather} blocks"
+                                       + ("" if args.no_overlap else " overlapped with the next frame")
+                                       if nranks > 1 else "one device")},
+            "ranks": nranks,
+            "group": {"kind": kind[topo["mode"]], "transport": transport, "rccl_ranks": info["nranks"]
+                      if transport == "rccl" else None, "overlap": not args.no_overlap, "devices": topo["devices"]
+                      if topo["mode"] == "group" else None},
+            "hip_runtime": hip_runtime_label(topo["mode"]),
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
             "segments_per_frame": int(segs_all / args.steps),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
-            "kernel_launches_per_frame": round(launches / args.steps, 2),
-            "kernel_timing": ("HIP events around each launch on the render stream, in the timed region" if live_events
-                              else "HIP events around each launch on the render stream, in an untimed re-render of "
-                                   "the timed frames (N > 1: kept out of the timed steps)"),
-            "ref_stack": {"overflow_segments": tot["ref_stack_overflow_segments"], "max": tot["ref_stack_max"],
-                          "note": "segments of the timed frames (this rank) that would write past the reference's "
-                                  "uint nodeStack[32] (pathTracer.comp:151), and the deepest stack they reach"},
-            "roofline": roofline(args, tot, avg_kernel_s, ms_per_step / 1e3),
+            "kernel_launches_per_frame": round(sum(a["launches"] for a in allr) / max(1, len(blocks)) / args.steps, 2),
+            "kernel_timing": ("HIP events around each render on the render stream, in the timed region" if live_events
+                              else "HIP events around each render on each rank's render stream, in an untimed "
+                                   "re-render of the timed frames (N > 1: kept out of the timed steps); the slowest "
+                                   "rank's average"),
+            "ref_stack": {"overflow_segments": T["ref_stack_overflow_segments"], "max": T["ref_stack_max"],
+                          "note": "segments of the timed frames that would write past the reference's uint "
+                                  "nodeStack[32] (pathTracer.comp:151), and the deepest stack they reach"},
+            "roofline": roofline(args, T, avg_kernel_s, ms_per_step / 1e3),
         }
+        if nranks > 1:
+            out["per_rank_block_ms"] = [b["block_ms"] for b in blocks]
+            if distinct < nranks:
+                out["rehearsal"] = f"{nranks} ranks on {distinct} device(s): not a scaling measurement"
+        if spp > 1:
+            # samples 1..spp-1 shade their primary segment from sample 0's Intersect record (same ray): the reference
+            # executes those segments, this implementation does not (pathTracer.comp:309-310)
+            executed = segs_all - float(T["reused_primary_segments"])
+            out["executed_segments_per_frame"] = int(executed / args.steps)
+            out["executed_mrays_per_s"] = round(executed / elapsed_max / 1e6, 3)
+            out["value_note"] = ("value counts the reference's segments (Intersect calls of pathTracer.comp); "
+                                 "executed_* leaves out the primary segments of samples after the first, which reuse "
+                                 "sample 0's record")
         if verified is not None:
             out["verified"] = verified
-        if world == 1 and not args.no_cpu_baseline:
+        if nranks == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, W, H, spp, bounces, budget_s=args.cpu_seconds)
             out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
 
-    if world > 1:
-        ctx.set_gather_output(0, 0)
-        ctx.set_external_image(0, 0)
-    dev.free()
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    drv.close()
+    if rdzv is not None:
+        rdzv.close()
 
 
-def hip_runtime_label(world: int) -> str:
+def hip_runtime_label(mode: str) -> str:
     v = wcpt.runtime_version()
-    where = ("system /opt/rocm runtime (torch not imported)" if world == 1 else
+    where = ("the system /opt/rocm runtime (torch not imported)" if mode != "torch" else
              "the HIP runtime torch bundles (torch.distributed is imported first)")
     return f"HIP {v // 10000000}.{(v // 100000) % 100} ({v}), {where}"
 

@@ -35,8 +35,10 @@
 extern "C" {
 #endif
 
-/* 2: wcpt_counters gained ref_stack_overflow_segments / ref_stack_max; the wcpt_group_* multi-device entry points */
-#define WCPT_ABI_VERSION 2
+/* 2: wcpt_counters gained ref_stack_overflow_segments / ref_stack_max; the wcpt_group_* multi-device entry points.
+ * 3: groups overlap each frame's gather with the next frame's render; wcpt_group_create_ex (transports),
+ *    wcpt_group_unique_id / wcpt_group_create_rank (one process per device), wcpt_group_set_option, wcpt_group_info. */
+#define WCPT_ABI_VERSION 3
 
 /* ---- error codes (VkResult-compatible where a VkResult exists) ---------------------------------- */
 #define WCPT_SUCCESS                      0
@@ -69,9 +71,13 @@ extern "C" {
  * arithmetic, same results). 1 (default): rebuilt only when a draw's buffers were re-uploaded through
  * wcpt_buffer_upload / re-allocated, or its buffers or index count changed; the draw commands themselves are read
  * from the context's host copy of what wcpt_buffer_upload wrote (bytes never uploaded are read from the device).
- * 0: the draw commands are read from the device and the records rebuilt on every render (use this when the
- * application writes draw-command, vertex or index buffers by other means, e.g. hipMemcpy to a
- * wcpt_buffer_device_address or its own kernels: with 1, such writes into uploaded ranges are not seen). */
+ * The same cache holds what the runtime learns about each draw's BVH buffer (whether every leaf is small and lies on
+ * the derived records, which selects the wavefront's fast leaf layout); it is re-learned when the BVH buffer is
+ * re-uploaded through wcpt_buffer_upload or re-allocated.
+ * 0: the draw commands are read from the device, the records rebuilt on every render and the fast leaf layout is not
+ * used (use this when the application writes draw-command, vertex, index or BVH buffers by other means, e.g. hipMemcpy
+ * to a wcpt_buffer_device_address, a refit or its own kernels: with 1, such writes into uploaded ranges are not
+ * seen). A BVH rewritten behind the cache can give a wrong image but never a read outside the derived records. */
 #define WCPT_OPTION_TRIANGLE_CACHE 5
 /* Megakernel leaf tests: -1 (default) choose by mean triangles per leaf; 0 single records; 1 pair records
  * (two triangles per lane with packed-FP32 arithmetic). Results are identical either way. */
@@ -292,33 +298,74 @@ int      wcpt_render_counters(wcpt_context* ctx, const wcpt_scene_data* scene, u
  * (s_memtime cycles summed over waves): {fetch, leaf, interior, pop, epilogue, waves, iterations, -}. */
 int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
 
-/* ---- one frame on several devices from one host thread ------------------------------- */
+/* ---- one frame on several devices ------------------------------------------------------- */
 /* The reference host is one process and one thread (main.jai:185-194) driving Render (PathTracingRenderer.jai:399).
  * A group keeps that shape for N devices: one context per device, rank r rendering rows [r*H/N, (r+1)*H/N) of the
- * frame with unchanged global pixel indices and seeds (so the frame equals a one-device render bit for bit), and an
- * RCCL communicator over the devices (ncclCommInitAll, rccl.h:236) for the one exchange: each frame's row blocks
- * go to the root device over xGMI as grouped ncclSend/ncclRecv (rccl.h:700,722; blocks may differ by a row).
- *   wcpt_group_create      devices[0..n) distinct device ordinals; `root` is the rank that receives the frame.
- *   wcpt_group_context     rank r's context: upload that device's copy of the scene with wcpt_buffer_* and set
- *                          kernels/options on it, as for a single context. Owned by the group.
+ * frame with unchanged global pixel indices and seeds (so the frame equals a one-device render bit for bit), and one
+ * exchange per presented frame: the row blocks go to the root device over xGMI (blocks may differ by a row).
+ *   wcpt_group_create      one process, one thread, devices[0..n) distinct device ordinals, RCCL transport
+ *                          (ncclCommInitAll, rccl.h:236; grouped ncclSend/ncclRecv, rccl.h:700,722). `root` is the
+ *                          rank that receives the frame.
+ *   wcpt_group_create_ex   the same with a transport: WCPT_GROUP_TRANSPORT_RCCL, or WCPT_GROUP_TRANSPORT_COPY
+ *                          (hipMemcpyPeerAsync of each block into the root's frame, on the sending device's copy
+ *                          path; a device may then be listed more than once, so an N-rank group can be rehearsed on
+ *                          fewer devices: every rank still has its own context, streams and payloads).
+ *   wcpt_group_unique_id / wcpt_group_create_rank   one process per device (e.g. one process per GPU under
+ *                          torchrun): the root's process makes the id (ncclGetUniqueId), the host hands its 128 bytes
+ *                          to every process, and each process creates its rank (ncclCommInitRank). RCCL only. All
+ *                          processes then make the same wcpt_group_* calls in the same order (collective).
+ *   wcpt_group_context     rank r's context (NULL for a rank of another process): upload that device's copy of the
+ *                          scene with wcpt_buffer_* and set kernels/options on it, as for a single context. Owned by
+ *                          the group.
  *   wcpt_group_create_screen  CreateScreen/Resize for the whole frame (each rank allocates only its row block).
  *   wcpt_group_set_output  where the presented frame goes: device memory on the root device (e.g.
  *                          wcpt_buffer_device_address of a root-context buffer) of width*height*(payload bytes per
  *                          pixel), row-major, in WCPT_PAYLOAD_* format; dst == 0 turns presenting off (the ranks
- *                          keep accumulating their blocks). The root renders its own block straight into it; the
- *                          other ranks' renders write their blocks into group-owned payload buffers (no copy pass).
- *   wcpt_group_render      Render on every rank (scene by value; materials/spheres/draw_commands are arrays of n
- *                          device addresses, rank r's in [r]), then, with an output set, the gather of this frame on
- *                          the ranks' streams. Asynchronous, like wcpt_render.
- *   wcpt_group_sync        waits for every rank (and reports a traversal-stack overflow on any of them).
- * Errors leave the group usable; wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains them. */
+ *                          keep accumulating their blocks). In a process that does not hold the root, only `format`
+ *                          is read (0 = off) and must equal the root's. The root renders its own block straight into
+ *                          the output; the other ranks' renders write their blocks into group-owned payload buffers
+ *                          (no copy pass).
+ *   wcpt_group_render      Render on every rank of this process (scene by value; materials/spheres/draw_commands are
+ *                          arrays of one device address per local rank, in rank order), then, with an output set,
+ *                          the gather of this frame. Asynchronous, like wcpt_render. Every rank's arguments are
+ *                          checked before any rank renders, so an argument error leaves every rank's accumulation as
+ *                          it was. With WCPT_GROUP_OPTION_OVERLAP (default 1) each rank's transfer runs on a
+ *                          communication stream of its own, ordered after that rank's render by an event, while the
+ *                          next frame renders into a second payload buffer; a render waits (on the device, not the
+ *                          host) only for the transfer that last read the payload it rewrites. 0: transfers run on
+ *                          the render streams, in line with the renders.
+ *   wcpt_group_sync        waits for every local rank's renders and transfers (and reports a traversal-stack
+ *                          overflow on any of them). The presented frame is complete after it.
+ * Errors leave the group usable, except a transport failure inside a posted exchange: the group then aborts its
+ * communicators and every later call but wcpt_group_destroy returns WCPT_ERROR_DEVICE_LOST.
+ * wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains an error. */
 /* The row-block split itself, for a host that runs one process per device (then wcpt_set_row_range with the
  * result): rank r of n renders rows [r*height/n, (r+1)*height/n). Host-only, no device needed. */
 int           wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uint32_t* rows);
 typedef struct wcpt_group wcpt_group;
+#define WCPT_GROUP_TRANSPORT_RCCL 0
+#define WCPT_GROUP_TRANSPORT_COPY 1
+#define WCPT_GROUP_UNIQUE_ID_BYTES 128   /* == sizeof(ncclUniqueId) (rccl.h NCCL_UNIQUE_ID_BYTES) */
+#define WCPT_GROUP_OPTION_OVERLAP 1
+typedef struct wcpt_group_info {
+    int32_t nranks;            /* ranks of the group; RCCL: ncclCommCount of this process's first communicator */
+    int32_t local_ranks;       /* ranks driven by this process */
+    int32_t first_local_rank;
+    int32_t root;
+    int32_t transport;         /* WCPT_GROUP_TRANSPORT_* */
+    int32_t overlap;           /* WCPT_GROUP_OPTION_OVERLAP */
+    int32_t distinct_devices;  /* distinct devices among this process's ranks */
+    int32_t broken;            /* 1 after a transport failure aborted the communicators */
+    uint64_t frames;           /* frames rendered (and, with an output set, gathered) */
+} wcpt_group_info;
 int           wcpt_group_create(const int* devices, int n, int root, wcpt_group** out);
+int           wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcpt_group** out);
+int           wcpt_group_unique_id(uint8_t* id /* WCPT_GROUP_UNIQUE_ID_BYTES */);
+int           wcpt_group_create_rank(int device, int nranks, int rank, int root, const uint8_t* id, wcpt_group** out);
 int           wcpt_group_destroy(wcpt_group* g);
 wcpt_context* wcpt_group_context(wcpt_group* g, int rank);
+int           wcpt_group_set_option(wcpt_group* g, int option, int value);
+int           wcpt_group_info_get(wcpt_group* g, wcpt_group_info* out);
 int           wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height);
 int           wcpt_group_set_output(wcpt_group* g, int format, uint64_t dst, uint64_t bytes);
 int           wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_t* materials,

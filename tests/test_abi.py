@@ -29,7 +29,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert wcpt.lib.wcpt_abi_version() == wcpt._lib.ABI_VERSION == 2
+    assert wcpt.lib.wcpt_abi_version() == wcpt._lib.ABI_VERSION == 3
 
 
 def test_option_and_kernel_constants_match_header():
@@ -131,11 +131,32 @@ def test_group_entry_points_reject_bad_arguments():
     assert lib.wcpt_group_create_screen(None, 8, 8) == -1001
     assert lib.wcpt_group_set_output(None, 4, 0, 0) == -1001
     assert lib.wcpt_group_sync(None) == -1001
+    assert lib.wcpt_group_create_ex(devs, 2, 0, 7, C.byref(h)) == -1000  # unknown transport
+    assert lib.wcpt_group_create_rank(0, 2, 2, 0, None, C.byref(h)) == -1000  # rank outside the group
+    assert lib.wcpt_group_create_rank(0, 2, 1, 0, None, C.byref(h)) == -1000  # N > 1 needs the unique id
+    assert lib.wcpt_group_create_rank(0, 2, 0, 3, None, C.byref(h)) == -1000  # root outside the group
+    assert lib.wcpt_group_set_option(None, 1, 1) == -1001
+    assert lib.wcpt_group_info_get(None, None) == -1001
+    assert lib.wcpt_group_render(None, None, None, None, None) == -1001
     if wcpt.device_count() == 0:
         assert lib.wcpt_group_create(devs, 1, 0, C.byref(h)) == -3     # WCPT_ERROR_INITIALIZATION_FAILED
+        assert lib.wcpt_group_create_ex(devs, 2, 0, 1, C.byref(h)) == -3
+        assert lib.wcpt_group_create_rank(0, 1, 0, 0, None, C.byref(h)) == -3
         assert not h.value
         with pytest.raises(wcpt.WcptError):
             wcpt.Group([0])
+
+
+def test_group_constants_match_header():
+    """Transport / option numbers and the info struct of the group API are the header's."""
+    text = open(HEADER).read()
+    for name, value in re.findall(r"#define WCPT_GROUP_(\w+?)\s+(\d+)", text):
+        assert getattr(wcpt._lib, "GROUP_" + name) == int(value), name
+    fields = re.search(r"typedef struct wcpt_group_info \{(.*?)\} wcpt_group_info;", text, re.S).group(1)
+    fields = re.sub(r"/\*.*?\*/", "", fields, flags=re.S)
+    names = re.findall(r"(?:int32_t|uint64_t)\s+(\w+);", fields)
+    assert names == [n for n, _ in wcpt._lib.GroupInfo._fields_]
+    assert C.sizeof(wcpt._lib.GroupInfo) == 8 * 4 + 8
 
 
 def test_runtime_version_reported():

@@ -1,0 +1,133 @@
+"""bench.py's host logic on CPU: which ranks a launch drives (--gpus against WORLD_SIZE, --devices, transports), the
+moving-camera frame sequence, and the torch-free rendezvous the one-process-per-GPU mode uses.
+The GPU side of the same paths is tests/test_gpu_multi.py."""
+import argparse
+import multiprocessing as mproc
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from wcpt.rdzv import Rendezvous  # noqa: E402
+
+
+def _topo(argv, env=None):
+    return bench.resolve_topology(bench.parse_args(argv), env or {})
+
+
+def test_gpus_flag_drives_a_one_process_group():
+    t = _topo([])
+    assert t == {"mode": "group", "nranks": 1, "rank": 0, "local_rank": 0, "devices": [0]}
+    t = _topo(["--gpus", "8"])
+    assert t["mode"] == "group" and t["nranks"] == 8 and t["devices"] == list(range(8))
+    t = _topo(["--gpus", "4", "--devices", "0,0,0,0", "--transport", "copy"])
+    assert t["devices"] == [0, 0, 0, 0]
+    with pytest.raises(SystemExit):
+        _topo(["--gpus", "4", "--devices", "0,0,0,0"])            # RCCL: one rank per device
+    with pytest.raises(SystemExit):
+        _topo(["--gpus", "3", "--devices", "0,1"])                # a device per rank
+    with pytest.raises(SystemExit):
+        _topo(["--gpus", "0"])
+    with pytest.raises(SystemExit):
+        _topo(["--dist-backend", "gloo"])                          # torch.distributed needs a launcher
+
+
+def test_under_torchrun_gpus_must_equal_world_size():
+    env = {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29500"}
+    t = _topo(["--gpus", "4"], env)
+    assert t == {"mode": "ranks", "nranks": 4, "rank": 2, "local_rank": 2, "devices": [2]}
+    assert _topo([], env)["mode"] == "ranks"                       # --gpus omitted: WORLD_SIZE decides
+    assert _topo(["--dist-backend", "gloo"], env)["mode"] == "torch"
+    with pytest.raises(SystemExit):
+        _topo(["--gpus", "8"], env)                                # the driver's N and the launcher's must agree
+    with pytest.raises(SystemExit):
+        _topo(["--gpus", "4", "--devices", "0,1,2,3"], env)
+
+
+def test_main_refuses_a_mismatched_launch_before_touching_a_device(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    with pytest.raises(SystemExit):
+        bench.main(["--gpus", "1"])
+
+
+def test_orbit_frames_move_the_camera_and_restart_accumulation():
+    import wcpt
+    from wcpt import scene as wscene
+    s = wscene.generate("cornell")
+    fs = bench.FrameSource(s, 64, 36, 4, 1, "orbit", 5)
+    sds = [fs.copy(k) for k in range(5)]
+    assert all(int(sd["renderedFramesCount"]) == 0 for sd in sds)   # editor.jai:149-150 while moving
+    pos = np.array([sd["position"] for sd in sds])
+    step = np.linalg.norm(np.diff(pos, axis=0), axis=1)
+    assert np.allclose(step, 4.0 * bench.ORBIT_DT, rtol=1e-4)       # MovementSpeed = 4 * deltaTime (editor.jai:91)
+    assert not np.array_equal(sds[0]["inverseView"], sds[1]["inverseView"])
+    cam = bench.orbit_camera(s.camera, 3)
+    assert cam.yaw == pytest.approx(s.camera.yaw - 3 * bench.ORBIT_YAW_DEG)
+    # back and forth: the camera stays within one half period's travel of where it started
+    far = max(np.linalg.norm(np.array(bench.orbit_camera(s.camera, k).position) - np.array(s.camera.position))
+              for k in range(0, 200, 5))
+    assert far <= bench.ORBIT_HALF_PERIOD * 4.0 * bench.ORBIT_DT * 1.01   # (float32 positions drift slightly)
+    still = bench.FrameSource(s, 64, 36, 4, 1, "still", 5)
+    assert [int(still.copy(k)["renderedFramesCount"]) for k in range(4)] == [0, 1, 2, 3]
+    assert np.array_equal(still.copy(3)["position"], sds[0]["position"])
+    assert wcpt.SCENE_DATA_DTYPE == sds[0].dtype
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rdzv_worker(rank, world, port, q):
+    with Rendezvous(rank, world, "127.0.0.1", port, timeout=60) as rz:
+        uid = rz.broadcast(bytes(range(128)) if rank == 0 else None)
+        rz.barrier()
+        got = rz.gather_obj({"rank": rank, "elapsed": 0.5 + rank})
+        every = rz.allgather_obj(rank * rank)
+        q.put((rank, uid, got, every))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rendezvous_broadcast_gather_barrier(world):
+    """The host exchanges of the one-process-per-GPU bench: the root's 128-byte RCCL id reaches every rank, per-rank
+    objects gather to rank 0 in rank order (the max-over-ranks time is taken from them), barriers return."""
+    ctx = mproc.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rdzv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, uid, got, every = q.get(timeout=60)
+        res[r] = (uid, got, every)
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in range(world):
+        uid, got, every = res[r]
+        assert uid == bytes(range(128))
+        assert every == [k * k for k in range(world)]
+        assert (got is None) == (r != 0)
+    assert [g["rank"] for g in res[0][1]] == list(range(world))
+    assert max(g["elapsed"] for g in res[0][1]) == 0.5 + world - 1
+
+
+def test_rendezvous_from_env_uses_master_port_plus_one(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    rz = Rendezvous.from_env()
+    assert rz.world == 1 and rz.broadcast(b"x") == b"x" and rz.gather(b"y") == [b"y"]
+    rz.barrier()
+    with pytest.raises(ValueError):
+        Rendezvous(2, 2)
+    assert isinstance(bench.parse_args([]), argparse.Namespace)

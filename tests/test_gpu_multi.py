@@ -1,12 +1,15 @@
 """Multi-device paths on the GPU box, through the product library:
 
-- the C-ABI group (wcpt_group_*: one context per device from one host thread, row blocks, RCCL gather of each presented
-  frame to the root) at n = 1, bit-identical to a plain context, in every payload format; its error paths;
+- the C-ABI group (wcpt_group_*: one context per rank from one host thread, row blocks, a gather of each presented frame
+  to the root) at n = 1, bit-identical to a plain context, in every payload format; its error paths;
+- the same group at n = 2..4 on the one GPU with the COPY transport (every rank its own context, streams, double-buffered
+  payloads and overlap events; only the wire differs from RCCL's), bit-identical to one context, overlapped and in line,
+  across resizes, and atomic when one rank's arguments are bad;
 - two ranks with libwcpt.so each rendering their row block of the frame on the one GPU, gathered over gloo (RCCL refuses
   two ranks on one device), against a one-context render.
 
-The N = 8 RCCL run itself is the driver's scaling bench (bench.py over torch.distributed); the group's N > 1 send/recv
-path needs distinct devices and is not reachable on a one-GPU box.
+The RCCL send/recv of an N > 1 group needs N distinct devices: the driver's scaling bench runs it (bench.py --gpus N, or
+one process per GPU under torchrun); a one-GPU box cannot.
 """
 import os
 import socket
@@ -227,3 +230,156 @@ def test_two_ranks_display_payload_gather_equals_oracle_composite(gpu_ctx, tmp_p
     _, want = oracle.composite(acc)
     assert got.dtype == np.uint8 and got.shape == (H, W, 4)
     assert np.array_equal(got, want)
+
+
+# ---- N-rank groups on the one GPU (COPY transport) --------------------------------------------------------------------
+COPY = wcpt._lib.GROUP_TRANSPORT_COPY
+
+
+def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4):
+    """Progressive frames through an n-rank COPY group on device 0: (presented frame bytes, each rank's block)."""
+    with wcpt.Group([0] * n, root=0, transport=COPY) as g:
+        devs = []
+        for r in range(n):
+            c = g.context(r)
+            c.set_kernel(kernel)
+            devs.append(wcpt.DeviceScene(c, s))
+        g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 1 if overlap else 0)
+        g.create_screen(W, H)
+        root = g.context(0)
+        nbytes = W * H * PB[fmt]
+        out = root.buffer_from(np.full(nbytes // 4, -5.0, np.float32))
+        g.set_output(fmt, root.buffer_address(out), nbytes)
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        for f in frames:
+            g.render(s.scene_data(W, H, max_bounce=bounces, frame=f), *addr)
+        g.sync()
+        info = g.info()
+        raw = root.buffer_download(out, nbytes)
+        blocks = [g.context(r).readback() for r in range(n)]
+        root.buffer_free(out)
+        for d in devs:
+            d.free()
+    assert info["frames"] == len(frames) and info["local_ranks"] == n and info["nranks"] == n
+    assert info["transport"] == COPY and info["distinct_devices"] == 1 and info["broken"] == 0
+    return raw, blocks
+
+
+def _as_frame(raw, fmt, W, H):
+    if fmt == wcpt._lib.PAYLOAD_DISPLAY_RGBA8:
+        return np.frombuffer(raw, np.uint8).reshape(H, W, 4)
+    return np.frombuffer(raw, np.float32).reshape(H, W, 4 if fmt == wcpt._lib.PAYLOAD_RGBA32F else 3)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+@pytest.mark.parametrize("fmt", [wcpt._lib.PAYLOAD_RGB32F, wcpt._lib.PAYLOAD_RGBA32F, wcpt._lib.PAYLOAD_DISPLAY_RGBA8])
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_group_of_n_ranks_equals_one_device(gpu_ctx, n, fmt, kernel):
+    """An n-rank group (one host thread, n contexts) presents, frame after frame, the one-device frame bit for bit:
+    every rank renders its row block with the global seeds, payload buffers alternate between frames while the previous
+    frame's transfer is in flight, and the blocks land at their rows of the root's output. Each rank keeps only its
+    block of the accumulation, equal to those rows of the one-device image."""
+    s = get_scene("cornell")
+    W, H, frames = 72, 45, (0, 1, 2, 3)
+    ref = _context_frames(s, W, H, frames, kernel=kernel)
+    raw, blocks = _group_frames(s, W, H, frames, n, fmt, kernel)
+    got = _as_frame(raw, fmt, W, H)
+    if fmt == wcpt._lib.PAYLOAD_DISPLAY_RGBA8:
+        assert np.array_equal(got, oracle.composite(ref)[1])
+    else:
+        assert np.array_equal(got.view(np.uint32), ref[..., :got.shape[2]].view(np.uint32))
+    from wcpt.dist import row_block
+    for r, blk in enumerate(blocks):
+        y0, rows = row_block(H, n, r)
+        assert np.array_equal(blk.view(np.uint32), ref[y0:y0 + rows].view(np.uint32))
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_group_overlapped_and_inline_gathers_agree(gpu_ctx, kernel):
+    """WCPT_GROUP_OPTION_OVERLAP on (communication streams, double-buffered payloads) and off (transfers in line with
+    the renders) present the same bytes over many frames, and both equal the oracle's accumulated frame."""
+    s = get_scene("default_dielectric")
+    W, H, frames = 40, 27, tuple(range(9))
+    a, _ = _group_frames(s, W, H, frames, 3, wcpt._lib.PAYLOAD_RGBA32F, kernel, overlap=True, bounces=3)
+    b, _ = _group_frames(s, W, H, frames, 3, wcpt._lib.PAYLOAD_RGBA32F, kernel, overlap=False, bounces=3)
+    assert a == b
+    acc = None
+    for f in frames:
+        acc, _ = oracle.render_scene(s, W, H, max_bounce=3, frame=f, image=acc, threads=8)
+    assert_close(_as_frame(a, wcpt._lib.PAYLOAD_RGBA32F, W, H).copy(), acc)
+
+
+def test_group_rank_with_bad_arguments_renders_nothing(gpu_ctx):
+    """A frame whose rank-1 arguments are invalid (a draw command whose indexCount exceeds its index buffer) is refused
+    before any rank renders: the error comes back, no accumulation advances, the group stays usable, and the frames
+    that follow equal a one-device sequence without the refused frame. Destroying the group afterwards does not hang."""
+    s = get_scene("cornell")
+    W, H = 48, 30
+    with wcpt.Group([0, 0, 0], transport=COPY) as g:
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(3)]
+        g.create_screen(W, H)
+        root = g.context(0)
+        out = root.buffer_alloc(W * H * 16)
+        g.set_output(wcpt._lib.PAYLOAD_RGBA32F, root.buffer_address(out), W * H * 16)
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        g.render(s.scene_data(W, H, max_bounce=4, frame=0), *addr)
+        c1 = g.context(1)
+        bad_draws = np.zeros(1, dtype=wcpt.DRAW_COMMAND_DTYPE)
+        m = s.meshes[0]
+        vb, ib, nb = (c1.buffer_from(m.positions), c1.buffer_from(m.indices), c1.buffer_from(m.nodes))
+        bad_draws[0] = (c1.buffer_address(vb), c1.buffer_address(ib), c1.buffer_address(nb), m.indices.size + 300, 0)
+        bd = c1.buffer_from(bad_draws)
+        bad = [list(x) for x in addr]
+        bad[2][1] = c1.buffer_address(bd)
+        with pytest.raises(wcpt.WcptError) as e:
+            g.render(s.scene_data(W, H, max_bounce=4, frame=1), *bad)
+        assert e.value.code == -1000
+        assert g.info()["broken"] == 0 and g.info()["frames"] == 1
+        for f in (1, 2):
+            g.render(s.scene_data(W, H, max_bounce=4, frame=f), *addr)
+        g.sync()
+        got = np.frombuffer(root.buffer_download(out, W * H * 16), np.float32).reshape(H, W, 4)
+        for b in (vb, ib, nb, bd):
+            c1.buffer_free(b)
+        root.buffer_free(out)
+        for d in devs:
+            d.free()
+    ref = _context_frames(s, W, H, (0, 1, 2))
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_group_resize_regrows_payloads_without_device_sync(gpu_ctx):
+    """Resizing a 2-rank overlapped group to a larger frame regrows each sender's payload buffers with the stream-ordered
+    allocator while earlier transfers may still be queued; an output too small for the new frame is refused and
+    presenting stops until a new one is set; the next frames equal the one-device frames of the new size."""
+    s = get_scene("cornell")
+    with wcpt.Group([0, 0], transport=COPY) as g:
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(2)]
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        root = g.context(0)
+        results = []
+        prev = None
+        for (W, H) in ((32, 20), (80, 50), (24, 9)):
+            nbytes = W * H * 12
+            out = root.buffer_alloc(nbytes)
+            if prev is not None and W * H > prev[1]:
+                with pytest.raises(wcpt.WcptError):
+                    g.create_screen(W, H)           # the previous output is too small: presenting stops
+                assert g.info()["frames"] == 2 * len(results)
+            else:
+                g.create_screen(W, H)
+            g.set_output(wcpt._lib.PAYLOAD_RGB32F, root.buffer_address(out), nbytes)
+            if prev is not None:
+                root.buffer_free(prev[0])
+            prev = (out, W * H)
+            for f in (0, 1):
+                g.render(s.scene_data(W, H, max_bounce=4, frame=f), *addr)
+            g.sync()
+            results.append((W, H, np.frombuffer(root.buffer_download(out, nbytes), np.float32).reshape(H, W, 3)))
+        g.set_output(wcpt._lib.PAYLOAD_RGB32F, 0, 0)
+        root.buffer_free(prev[0])
+        for d in devs:
+            d.free()
+    for W, H, got in results:
+        ref = _context_frames(s, W, H, (0, 1))
+        assert np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32)), (W, H)

@@ -125,3 +125,32 @@ def test_reference_stack_overflow_counted_alike():
     assert rc["ref_stack_max"] == int(gc["ref_stack_max"].max()) == 41
     assert rc["ref_stack_overflow_segments"] > 0
     assert rc["ref_stack_overflow_segments"] == int(gc["ref_stack_overflow_segments"].sum())
+
+
+FULL_SIZE = [  # BASELINE configs at their full 1920x1080 size (bench.py CONFIGS): scene, maxBounceCount, frames
+    ("c2", "cornell", 4, (0, 1)),
+    ("c3", "atrium", 4, (0,)),
+    ("ref", "reference_init", 3, (0,)),
+]
+FULL_ROWS = [k * 1080 // 8 + 67 for k in range(8)]  # one row in each eighth of the frame (the 8-GPU row blocks)
+
+
+@pytest.mark.parametrize("cfg,name,b,frames", FULL_SIZE, ids=[c[0] for c in FULL_SIZE])
+def test_restatement_agrees_at_headline_size(cfg, name, b, frames):
+    """the binary32 restatement against the C oracle on rows of the full 1920x1080 frames of the
+    benchmarked configs, one row in each eighth of the frame. Per row band: <= 0.5 % of pixels diverged (|d| > 1e-4),
+    >= 90 % of channels bit-identical, every work counter within 0.5 %."""
+    s = _scene(name)
+    W, H = 1920, 1080
+    for y in FULL_ROWS:
+        ref = got = None
+        for f in frames:
+            ref, rc = oracle.render_scene(s, W, H, max_bounce=b, frame=f, y0=y, rows=1, image=ref)
+            got, gc = pt_f64.render_scene(s, W, H, max_bounce=b, frame=f, y0=y, rows=1, image=got, dtype=np.float32)
+        diff = np.abs(got[..., :3].astype(np.float64) - ref[..., :3].astype(np.float64)).max(axis=2)
+        bad = ~(diff <= 1e-4)
+        assert bad.mean() <= 0.005, (cfg, y, int(bad.sum()))
+        assert np.mean(got[..., :3] == ref[..., :3]) >= 0.90, (cfg, y)
+        for k in ("segments", "node_pops", "interior_visits", "triangle_tests", "sphere_tests", "hits"):
+            g, r = int(gc[k].sum()), int(rc[k])
+            assert abs(g - r) <= 0.005 * max(1, r), (cfg, y, k, g, r)

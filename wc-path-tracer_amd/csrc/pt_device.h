@@ -755,6 +755,24 @@ __device__ __forceinline__ uint32_t leaf_record_off(uint32_t first, uint32_t cou
     const uint32_t k = leaf_record(first, count, ntri);
     return (k != kNoRecord && k < (1u << 26)) ? k * 48u : kNoRecord;
 }
+/* Single records through a buffer resource of ntri records (48 B each; ntri < 2^24 / 3 for the draws that use it):
+ * an offset past the records reads zeros (hardware range check), i.e. a = e1 = e2 = 0, whose det is 0 and whose test
+ * never accepts (0 * inf = NaN fails every comparison) */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tri_rsrc(gtri_ptr t, uint32_t ntri)
+{
+    return __builtin_amdgcn_make_buffer_rsrc((void*)t, (short)0, (int)(ntri * 48u), kBufferDword3);
+}
+__device__ __forceinline__ TriE load_tri_rsrc(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const v4f r0 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    const v4f r1 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
+    const v4f r2 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, off + 32, 0, 0));
+    TriE e;
+    e.a = mk3(r0.x, r0.y, r0.z);
+    e.e1 = mk3(r0.w, r1.x, r1.y);
+    e.e2 = mk3(r1.z, r1.w, r2.x);
+    return e;
+}
 __device__ __forceinline__ TriE load_tri_at(gtri_ptr t, uint32_t off)
 {
     const gtri_ptr q = reinterpret_cast<gtri_ptr>(reinterpret_cast<const WCPT_GLOBAL char*>(t) + off);

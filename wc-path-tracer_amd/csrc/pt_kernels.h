@@ -34,7 +34,7 @@ struct LaunchArgs {
     uint32_t mk_tile_order;      /* static megakernel: 0 XCD-banded, 1 scattered, 2 auto, 3-6 striped bands (WCPT_OPTION_MK_TILE_ORDER) */
     float4* image;
     float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
-    uint32_t wire_ch;            /* its channels per pixel: 3 or 4 */
+    uint32_t wire_ch;            /* its format (wcpt.h WCPT_PAYLOAD_*): 3 = RGB32F (12 B/px), 4 = RGBA32F (16 B/px), 8 = display RGBA8 (4 B/px) */
     uint32_t W, H, y0, rows;
     uint32_t* status;
     unsigned long long* counters;
@@ -161,7 +161,11 @@ hipError_t launch_selftest(int fn, const uint32_t* in, const uint32_t* in2, uint
 
 /* wcpt_runtime.hip internals used by the multi-device group (wcpt_group.hip) */
 hipStream_t context_stream(wcpt_context* ctx);
+int context_device(wcpt_context* ctx);
 int context_error(wcpt_context* ctx, int code, const char* msg);
+int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                    uint64_t draws);
+int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows);
 
 } // namespace wcpt
 

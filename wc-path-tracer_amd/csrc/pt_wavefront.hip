@@ -205,6 +205,7 @@ struct Geom {
     gf32_ptr vertices;
     uint32_t nodes;                /* BVH node count when the BVH is a known context buffer of < 2^24 nodes, else 0 */
     __amdgpu_buffer_rsrc_t rsrc;   /* buffer resource over those nodes (load_pair_rsrc) */
+    __amdgpu_buffer_rsrc_t trsrc;  /* buffer resource over the ntri single records (load_tri_rsrc; kTriFlagIndex24 draws) */
 };
 
 __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ draws,
@@ -221,6 +222,7 @@ __device__ __forceinline__ Geom load_geom(const wcpt_draw_command* __restrict__ 
     g.vertices = as_f32(draws[d].vertexBuffer);
     g.nodes = g.packed ? (uint32_t)(tri_records[kTriTableWords * d + 2u] >> 32) : 0u;
     g.rsrc = node_rsrc(g.bvh, g.nodes);
+    g.trsrc = tri_rsrc(g.tris, g.idx24 ? g.ntri : 0u);
     return g;
 }
 
@@ -503,7 +505,10 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
                 if (GEO == 2 && WCPT_WF_LEAF_RECORDS) {
-                    leaf_step(load_tri_at(g.tris, ca * 16u)); /* every leaf triangle has its record (kTriFlagLeafRecords) */
+                    /* every leaf triangle has its record (kTriFlagLeafRecords); the load goes through a buffer resource
+                     * bounded by the draw's records, so a BVH rewritten behind the runtime's cache (wcpt.h
+                     * WCPT_OPTION_TRIANGLE_CACHE) reads zeros -- a triangle no ray accepts -- instead of past them */
+                    leaf_step(load_tri_rsrc(g.trsrc, ca * 16u));
                 } else {
                     const uint32_t off = g.idx24 ? tri_record_off24(ca, g.lim3) : cr;
                     leaf_step(off != kNoRecord ? load_tri_at(g.tris, off) : index_tri());

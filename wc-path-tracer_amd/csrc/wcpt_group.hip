@@ -1,43 +1,79 @@
 /*
- * wcpt_group.hip — one frame on several devices from one host thread (include/wcpt.h wcpt_group_*).
+ * wcpt_group.hip — one frame on several devices (include/wcpt.h wcpt_group_*).
  *
  * The reference renders every frame on one device from one thread (src/main.jai:185-194 -> Render,
  * src/PathTracingRenderer.jai:399-457). Every pixel is independent -- its seed depends only on the global (x, y,
  * frame) (pathTracer.comp:304) and the accumulation is per pixel (:314-323) -- so the frame partitions into row
  * blocks: rank r of N renders rows [r*H/N, (r+1)*H/N) on its own device, keeps only that block of the accumulation
  * image, and the union is bit-identical to a one-device render. The one exchange is presenting a frame: the blocks
- * go to the root device. That is a gather of unequal blocks (H/N need not be an integer), issued as grouped
- * point-to-point ncclSend / ncclRecv on the ranks' render streams (rccl.h:700,722), so each transfer follows its
- * rank's render in stream order and xGMI carries the 7 incoming blocks of an 8-GPU node over 7 links at once.
- * The communicator is ncclCommInitAll (rccl.h:236): one process, one communicator per device, which is how a
- * single-threaded host like the reference's drives RCCL (every call on several communicators inside one
- * ncclGroupStart/ncclGroupEnd).
+ * go to the root device. That is a gather of unequal blocks (H/N need not be an integer).
  *
- * The payload is written by the render itself (wcpt_set_gather_output): the root renders its block straight into the
- * presented frame, the other ranks into a group-owned payload buffer on their device that the send reads.
+ * Two ways to hold the ranks:
+ *  - one process, one thread, all devices (wcpt_group_create[_ex]): the shape of the reference's host. RCCL transport:
+ *    ncclCommInitAll (rccl.h:236), one communicator per device, every frame's sends and receives inside one
+ *    ncclGroupStart/ncclGroupEnd (rccl.h:700,722); xGMI carries the 7 incoming blocks of an 8-GPU node over 7 links
+ *    at once. COPY transport: each rank pushes its block into the root's frame with hipMemcpyPeerAsync on its own
+ *    device's copy path; a device may be listed more than once (an N-rank rehearsal on fewer devices).
+ *  - one process per device (wcpt_group_create_rank): ncclCommInitRank with an id the host distributes; each process
+ *    holds its own rank and the gather is the same send/receive pattern.
+ *
+ * Overlap (WCPT_GROUP_OPTION_OVERLAP, default on). Each local rank has a render stream (its context's) and a
+ * communication stream. Frame k on a sending rank: the render writes the block into payload buffer k % 2
+ * (wcpt_set_gather_output: no copy pass), an event marks the render's end, the communication stream waits for it and
+ * sends, and an event marks the send's end; the render of frame k + 2, which rewrites that buffer, waits for that
+ * event on the device (hipStreamWaitEvent), so the host never blocks. The root renders its block straight into the
+ * presented frame and receives the others' rows on its communication stream, so its next render does not wait for the
+ * slowest rank's transfer. Payload buffers come from the stream-ordered allocator (hipMallocAsync on the render
+ * stream); a regrown buffer is released with hipFreeAsync on the communication stream after the last work that can
+ * touch it, so a resize never synchronises the device.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../include/wcpt.h"
 #include "pt_kernels.h"
 
+static_assert(sizeof(ncclUniqueId) == WCPT_GROUP_UNIQUE_ID_BYTES, "WCPT_GROUP_UNIQUE_ID_BYTES");
+
+namespace {
+
+constexpr int kPayloadBuffers = 2;
+
+/* One rank driven by this process. */
+struct LocalRank {
+    int rank = 0;
+    int device = 0;
+    wcpt_context* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    hipStream_t comm_stream = nullptr;
+    void* payload[kPayloadBuffers] = {};
+    uint64_t payload_cap[kPayloadBuffers] = {};
+    hipEvent_t ready[kPayloadBuffers] = {};  /* the render that wrote payload[b] has finished */
+    hipEvent_t sent[kPayloadBuffers] = {};   /* the transfer that read payload[b] has finished */
+    bool sent_pending[kPayloadBuffers] = {};
+    hipEvent_t fence = nullptr;              /* scratch: orders a stream-ordered free after the render stream */
+};
+
+} // namespace
+
 struct wcpt_group {
-    int n = 0;
+    int nranks = 0;
     int root = 0;
-    std::vector<int> devices;
-    std::vector<wcpt_context*> ctx;
-    std::vector<ncclComm_t> comm;      /* n > 1 only */
+    int transport = WCPT_GROUP_TRANSPORT_RCCL;
+    bool overlap = true;
+    bool broken = false;
+    std::vector<LocalRank> local;       /* this process's ranks, in rank order */
+    int root_local = -1;                /* index of the root in `local`, or -1 */
     uint32_t width = 0, height = 0;
-    std::vector<uint32_t> y0, rows;    /* row block of each rank */
-    int format = 0;                    /* WCPT_PAYLOAD_* of the presented frame; 0 = not presenting */
-    uint64_t dst = 0, dst_bytes = 0;   /* the presented frame on the root device */
-    std::vector<void*> payload;        /* rank r != root: its block's payload on its device */
-    std::vector<uint64_t> payload_cap;
+    int format = 0;                     /* WCPT_PAYLOAD_* of the presented frame; 0 = not presenting */
+    uint64_t dst = 0, dst_bytes = 0;    /* the presented frame on the root device (root's process only) */
+    uint64_t frames = 0;
 };
 
 namespace {
@@ -52,6 +88,24 @@ int group_error(int code, const char* fmt, ...)
     return wcpt::context_error(nullptr, code, buf);
 }
 
+int hip_fail(hipError_t e, const char* what)
+{
+    (void)hipGetLastError();
+    return group_error(e == hipErrorOutOfMemory ? WCPT_ERROR_OUT_OF_DEVICE_MEMORY : WCPT_ERROR_DEVICE_LOST, "%s: %s",
+                       what, hipGetErrorString(e));
+}
+
+#define GHIP(expr, what)                          \
+    do {                                          \
+        hipError_t _e = (expr);                   \
+        if (_e != hipSuccess) return hip_fail(_e, (what)); \
+    } while (0)
+
+int nccl_fail(ncclResult_t e, const char* what)
+{
+    return group_error(WCPT_ERROR_DEVICE_LOST, "%s: %s", what, ncclGetErrorString(e));
+}
+
 uint64_t pixel_bytes(int format) { return format == WCPT_PAYLOAD_DISPLAY_RGBA8 ? 4u : 4ull * (uint64_t)format; }
 
 bool valid_format(int f)
@@ -59,93 +113,236 @@ bool valid_format(int f)
     return f == WCPT_PAYLOAD_RGB32F || f == WCPT_PAYLOAD_RGBA32F || f == WCPT_PAYLOAD_DISPLAY_RGBA8;
 }
 
-/* Point every rank's render at its payload: the root's block of the presented frame, or the rank's own buffer
- * (grown on demand). format == 0 turns the payloads off. */
+void block_of(const wcpt_group* g, int rank, uint32_t& y0, uint32_t& rows)
+{
+    (void)wcpt_row_block(g->height, (uint32_t)g->nranks, (uint32_t)rank, &y0, &rows);
+}
+
+bool presenting(const wcpt_group* g) { return g->format != 0 && g->width != 0; }
+
+/* Release a payload buffer once every queued use of it is over: the render stream's work (a render writing it) is
+ * fenced into the communication stream, and the free follows the transfers there. */
+int release_payload(LocalRank& lr, int b)
+{
+    if (!lr.payload[b]) return WCPT_SUCCESS;
+    GHIP(hipSetDevice(lr.device), "hipSetDevice");
+    GHIP(hipEventRecord(lr.fence, wcpt::context_stream(lr.ctx)), "hipEventRecord(fence)");
+    GHIP(hipStreamWaitEvent(lr.comm_stream, lr.fence, 0), "hipStreamWaitEvent(fence)");
+    GHIP(hipFreeAsync(lr.payload[b], lr.comm_stream), "hipFreeAsync(payload)");
+    lr.payload[b] = nullptr;
+    lr.payload_cap[b] = 0;
+    lr.sent_pending[b] = false;
+    return WCPT_SUCCESS;
+}
+
+/* Size every sending rank's payload buffers for the current frame and format (stream-ordered: no device sync) and
+ * point the root's render at its block of the presented frame. Called after a screen or output change. */
 int attach_payloads(wcpt_group* g)
 {
-    for (int r = 0; r < g->n; r++) {
-        if (!g->format || !g->width) {
-            const int rc = wcpt_set_gather_output(g->ctx[r], 0, 0, 0);
+    for (LocalRank& lr : g->local) {
+        if (!presenting(g)) {
+            const int rc = wcpt_set_gather_output(lr.ctx, 0, 0, 0);
             if (rc) return rc;
             continue;
         }
-        const uint64_t bytes = (uint64_t)g->width * g->rows[r] * pixel_bytes(g->format);
-        uint64_t addr = 0;
-        if (r == g->root) {
-            addr = g->dst + (uint64_t)g->width * g->y0[r] * pixel_bytes(g->format);
-        } else {
-            if (g->payload_cap[r] < bytes) {
-                if (hipSetDevice(g->devices[r]) != hipSuccess) return group_error(WCPT_ERROR_DEVICE_LOST, "hipSetDevice");
-                if (g->payload[r]) {
-                    (void)hipDeviceSynchronize(); /* the previous payload may still be read by a send */
-                    (void)hipFree(g->payload[r]);
-                }
-                g->payload[r] = nullptr;
-                g->payload_cap[r] = 0;
-                if (hipMalloc(&g->payload[r], bytes) != hipSuccess)
-                    return group_error(WCPT_ERROR_OUT_OF_DEVICE_MEMORY, "hipMalloc(payload of rank %d, %llu bytes)", r,
-                                       (unsigned long long)bytes);
-                g->payload_cap[r] = bytes;
-            }
-            addr = reinterpret_cast<uint64_t>(g->payload[r]);
+        uint32_t y0 = 0, rows = 0;
+        block_of(g, lr.rank, y0, rows);
+        const uint64_t bytes = (uint64_t)g->width * rows * pixel_bytes(g->format);
+        if (lr.rank == g->root) {
+            const int rc = wcpt_set_gather_output(lr.ctx, g->dst + (uint64_t)g->width * y0 * pixel_bytes(g->format),
+                                                  bytes, (uint32_t)g->format);
+            if (rc) return rc;
+            continue;
         }
-        const int rc = wcpt_set_gather_output(g->ctx[r], addr, bytes, (uint32_t)g->format);
+        GHIP(hipSetDevice(lr.device), "hipSetDevice");
+        for (int b = 0; b < kPayloadBuffers; b++) {
+            if (lr.payload_cap[b] >= bytes) continue;
+            int rc = release_payload(lr, b);
+            if (rc) return rc;
+            GHIP(hipSetDevice(lr.device), "hipSetDevice");
+            const hipError_t e = hipMallocAsync(&lr.payload[b], bytes, wcpt::context_stream(lr.ctx));
+            if (e != hipSuccess) {
+                lr.payload[b] = nullptr;
+                (void)hipGetLastError();
+                return group_error(WCPT_ERROR_OUT_OF_DEVICE_MEMORY, "hipMallocAsync(payload of rank %d, %llu bytes): %s",
+                                   lr.rank, (unsigned long long)bytes, hipGetErrorString(e));
+            }
+            lr.payload_cap[b] = bytes;
+        }
+        /* the next render picks its buffer; park the output on buffer 0 meanwhile */
+        const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[0]), bytes,
+                                              (uint32_t)g->format);
         if (rc) return rc;
     }
     return WCPT_SUCCESS;
 }
 
-int nccl_fail(ncclResult_t e, const char* what)
+/* Set up everything a local rank needs beyond its context (created by the caller). */
+int init_local(LocalRank& lr)
 {
-    return group_error(WCPT_ERROR_DEVICE_LOST, "%s: %s", what, ncclGetErrorString(e));
+    GHIP(hipSetDevice(lr.device), "hipSetDevice");
+    GHIP(hipStreamCreateWithFlags(&lr.comm_stream, hipStreamNonBlocking), "hipStreamCreate(communication)");
+    for (int b = 0; b < kPayloadBuffers; b++) {
+        GHIP(hipEventCreateWithFlags(&lr.ready[b], hipEventDisableTiming), "hipEventCreate");
+        GHIP(hipEventCreateWithFlags(&lr.sent[b], hipEventDisableTiming), "hipEventCreate");
+    }
+    GHIP(hipEventCreateWithFlags(&lr.fence, hipEventDisableTiming), "hipEventCreate");
+    return WCPT_SUCCESS;
+}
+
+/* A transport failure inside a posted exchange: the communicators may hold half-matched operations, so abort them
+ * (their kernels are torn down) and refuse further frames. */
+int break_group(wcpt_group* g, int rc)
+{
+    g->broken = true;
+    for (LocalRank& lr : g->local)
+        if (lr.comm) {
+            (void)ncclCommAbort(lr.comm);
+            lr.comm = nullptr;
+        }
+    return rc;
+}
+
+int alloc_group(int nranks, int root, int transport, wcpt_group** out)
+{
+    wcpt_group* g = new (std::nothrow) wcpt_group();
+    if (!g) return group_error(WCPT_ERROR_OUT_OF_HOST_MEMORY, "out of host memory");
+    g->nranks = nranks;
+    g->root = root;
+    g->transport = transport;
+    *out = g;
+    return WCPT_SUCCESS;
+}
+
+int device_count()
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return count;
 }
 
 } // namespace
 
 extern "C" {
 
-int wcpt_group_create(const int* devices, int n, int root, wcpt_group** out)
+int wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcpt_group** out)
 {
     if (!out) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "null out");
     *out = nullptr;
     if (!devices || n < 1) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group of %d devices", n);
     if (root < 0 || root >= n) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "root %d outside [0,%d)", root, n);
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
-        (void)hipGetLastError();
-        return group_error(WCPT_ERROR_INITIALIZATION_FAILED, "no HIP device available");
-    }
+    if (transport != WCPT_GROUP_TRANSPORT_RCCL && transport != WCPT_GROUP_TRANSPORT_COPY)
+        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group transport %d", transport);
+    const int count = device_count();
+    if (count == 0) return group_error(WCPT_ERROR_INITIALIZATION_FAILED, "no HIP device available");
     for (int r = 0; r < n; r++) {
         if (devices[r] < 0 || devices[r] >= count)
             return group_error(WCPT_ERROR_INVALID_ARGUMENT, "device %d out of range [0,%d)", devices[r], count);
-        for (int q = 0; q < r; q++)
+        for (int q = 0; q < r && transport == WCPT_GROUP_TRANSPORT_RCCL; q++)
             if (devices[q] == devices[r])
-                return group_error(WCPT_ERROR_INVALID_ARGUMENT, "device %d listed twice (one rank per device)", devices[r]);
+                return group_error(WCPT_ERROR_INVALID_ARGUMENT,
+                                   "device %d listed twice (RCCL: one rank per device; WCPT_GROUP_TRANSPORT_COPY allows it)",
+                                   devices[r]);
     }
-    wcpt_group* g = new (std::nothrow) wcpt_group();
-    if (!g) return group_error(WCPT_ERROR_OUT_OF_HOST_MEMORY, "out of host memory");
-    g->n = n;
-    g->root = root;
-    g->devices.assign(devices, devices + n);
-    g->ctx.assign(n, nullptr);
-    g->y0.assign(n, 0);
-    g->rows.assign(n, 0);
-    g->payload.assign(n, nullptr);
-    g->payload_cap.assign(n, 0);
+    wcpt_group* g = nullptr;
+    int rc = alloc_group(n, root, transport, &g);
+    if (rc) return rc;
+    g->local.resize(n);
+    g->root_local = root;
     for (int r = 0; r < n; r++) {
-        const int rc = wcpt_create(devices[r], &g->ctx[r]);
+        LocalRank& lr = g->local[r];
+        lr.rank = r;
+        lr.device = devices[r];
+        rc = wcpt_create(devices[r], &lr.ctx);
+        if (!rc) rc = init_local(lr);
         if (rc) {
             wcpt_group_destroy(g);
             return rc;
         }
     }
-    if (n > 1) {
-        g->comm.assign(n, nullptr);
-        const ncclResult_t e = ncclCommInitAll(g->comm.data(), n, devices);
+    if (n > 1 && transport == WCPT_GROUP_TRANSPORT_RCCL) {
+        std::vector<ncclComm_t> comms(n, nullptr);
+        const ncclResult_t e = ncclCommInitAll(comms.data(), n, devices);
         if (e != ncclSuccess) {
-            g->comm.clear();
             wcpt_group_destroy(g);
             return nccl_fail(e, "ncclCommInitAll");
+        }
+        for (int r = 0; r < n; r++) g->local[r].comm = comms[r];
+    }
+    if (n > 1 && transport == WCPT_GROUP_TRANSPORT_COPY) {
+        /* each sender writes into the root's frame: give its device access to the root's memory (xGMI peer access
+         * where the pair supports it; otherwise hipMemcpyPeerAsync stages the copy) */
+        for (int r = 0; r < n; r++) {
+            if (r == root || devices[r] == devices[root]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devices[r], devices[root]) == hipSuccess && can) {
+                (void)hipSetDevice(devices[r]);
+                const hipError_t e = hipDeviceEnablePeerAccess(devices[root], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                    wcpt_group_destroy(g);
+                    return hip_fail(e, "hipDeviceEnablePeerAccess");
+                }
+            }
+            (void)hipGetLastError();
+        }
+    }
+    *out = g;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_group_create(const int* devices, int n, int root, wcpt_group** out)
+{
+    return wcpt_group_create_ex(devices, n, root, WCPT_GROUP_TRANSPORT_RCCL, out);
+}
+
+int wcpt_group_unique_id(uint8_t* id)
+{
+    if (!id) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "null id");
+    ncclUniqueId u;
+    const ncclResult_t e = ncclGetUniqueId(&u);
+    if (e != ncclSuccess) return nccl_fail(e, "ncclGetUniqueId");
+    std::memcpy(id, &u, sizeof(u));
+    return WCPT_SUCCESS;
+}
+
+int wcpt_group_create_rank(int device, int nranks, int rank, int root, const uint8_t* id, wcpt_group** out)
+{
+    if (!out) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "rank %d of %d", rank, nranks);
+    if (root < 0 || root >= nranks) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "root %d outside [0,%d)", root, nranks);
+    if (nranks > 1 && !id) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "null unique id");
+    const int count = device_count();
+    if (count == 0) return group_error(WCPT_ERROR_INITIALIZATION_FAILED, "no HIP device available");
+    if (device < 0 || device >= count)
+        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "device %d out of range [0,%d)", device, count);
+    wcpt_group* g = nullptr;
+    int rc = alloc_group(nranks, root, WCPT_GROUP_TRANSPORT_RCCL, &g);
+    if (rc) return rc;
+    g->local.resize(1);
+    g->root_local = rank == root ? 0 : -1;
+    LocalRank& lr = g->local[0];
+    lr.rank = rank;
+    lr.device = device;
+    rc = wcpt_create(device, &lr.ctx);
+    if (!rc) rc = init_local(lr);
+    if (rc) {
+        wcpt_group_destroy(g);
+        return rc;
+    }
+    if (nranks > 1) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        (void)hipSetDevice(device);
+        const ncclResult_t e = ncclCommInitRank(&lr.comm, nranks, u, rank);
+        if (e != ncclSuccess) {
+            lr.comm = nullptr;
+            wcpt_group_destroy(g);
+            return nccl_fail(e, "ncclCommInitRank");
         }
     }
     *out = g;
@@ -155,25 +352,40 @@ int wcpt_group_create(const int* devices, int n, int root, wcpt_group** out)
 int wcpt_group_destroy(wcpt_group* g)
 {
     if (!g) return WCPT_SUCCESS;
-    for (int r = 0; r < g->n; r++)
-        if (g->ctx[r]) (void)wcpt_sync(g->ctx[r]);
-    for (ncclComm_t c : g->comm)
-        if (c) (void)ncclCommDestroy(c);
-    for (int r = 0; r < g->n; r++) {
-        if (g->payload[r]) {
-            (void)hipSetDevice(g->devices[r]);
-            (void)hipFree(g->payload[r]);
+    for (LocalRank& lr : g->local) {
+        if (lr.ctx) (void)wcpt_sync(lr.ctx);
+        if (lr.comm_stream) {
+            (void)hipSetDevice(lr.device);
+            (void)hipStreamSynchronize(lr.comm_stream);
         }
-        if (g->ctx[r]) wcpt_destroy(g->ctx[r]);
     }
+    for (LocalRank& lr : g->local)
+        if (lr.comm) (void)ncclCommDestroy(lr.comm);
+    for (LocalRank& lr : g->local) {
+        (void)hipSetDevice(lr.device);
+        for (int b = 0; b < kPayloadBuffers; b++) {
+            if (lr.payload[b] && lr.comm_stream) (void)hipFreeAsync(lr.payload[b], lr.comm_stream);
+            if (lr.ready[b]) (void)hipEventDestroy(lr.ready[b]);
+            if (lr.sent[b]) (void)hipEventDestroy(lr.sent[b]);
+        }
+        if (lr.fence) (void)hipEventDestroy(lr.fence);
+        if (lr.comm_stream) {
+            (void)hipStreamSynchronize(lr.comm_stream);
+            (void)hipStreamDestroy(lr.comm_stream);
+        }
+        if (lr.ctx) wcpt_destroy(lr.ctx);
+    }
+    (void)hipGetLastError();
     delete g;
     return WCPT_SUCCESS;
 }
 
 wcpt_context* wcpt_group_context(wcpt_group* g, int rank)
 {
-    if (!g || rank < 0 || rank >= g->n) return nullptr;
-    return g->ctx[rank];
+    if (!g) return nullptr;
+    for (LocalRank& lr : g->local)
+        if (lr.rank == rank) return lr.ctx;
+    return nullptr;
 }
 
 int wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uint32_t* rows)
@@ -186,28 +398,67 @@ int wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uin
     return WCPT_SUCCESS;
 }
 
+int wcpt_group_set_option(wcpt_group* g, int option, int value)
+{
+    if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    if (option != WCPT_GROUP_OPTION_OVERLAP) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "unknown group option %d", option);
+    const int rc = wcpt_group_sync(g); /* the streams' queued work follows the mode it was queued with */
+    if (rc) return rc;
+    g->overlap = value != 0;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_group_info_get(wcpt_group* g, wcpt_group_info* out)
+{
+    if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    if (!out) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "null info");
+    std::memset(out, 0, sizeof(*out));
+    out->nranks = g->nranks;
+    if (!g->local.empty() && g->local[0].comm) {
+        int c = 0;
+        const ncclResult_t e = ncclCommCount(g->local[0].comm, &c);
+        if (e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
+        out->nranks = c;
+    }
+    out->local_ranks = (int32_t)g->local.size();
+    out->first_local_rank = g->local.empty() ? -1 : g->local[0].rank;
+    out->root = g->root;
+    out->transport = g->transport;
+    out->overlap = g->overlap ? 1 : 0;
+    std::vector<int> seen;
+    for (const LocalRank& lr : g->local) {
+        bool dup = false;
+        for (int d : seen) dup |= d == lr.device;
+        if (!dup) seen.push_back(lr.device);
+    }
+    out->distinct_devices = (int32_t)seen.size();
+    out->broken = g->broken ? 1 : 0;
+    out->frames = g->frames;
+    return WCPT_SUCCESS;
+}
+
 int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
-    if (width == 0 || height < (uint32_t)g->n)
-        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "%ux%u frame for %d row blocks", width, height, g->n);
-    for (int r = 0; r < g->n; r++) {
-        /* the row-block split of SURVEY.md §8(e) (wcpt_row_block): blocks differ by at most one row */
-        uint32_t y0 = 0, rows = 0;
-        (void)wcpt_row_block(height, (uint32_t)g->n, (uint32_t)r, &y0, &rows);
-        const uint32_t y1 = y0 + rows;
-        /* a resized frame first keeps the previous block (clipped to the new height), so no rank ever allocates the
-         * whole frame; a fresh context takes its block before its first screen */
-        int rc = g->width ? wcpt_create_screen(g->ctx[r], width, height) : WCPT_SUCCESS;
-        if (!rc) rc = wcpt_set_row_range(g->ctx[r], y0, y1 - y0);
-        if (!rc) rc = wcpt_create_screen(g->ctx[r], width, height); /* zeroes the block (CreateScreen) */
-        if (rc) return rc;
-        g->y0[r] = y0;
-        g->rows[r] = y1 - y0;
-    }
+    if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
+    if (width == 0 || height < (uint32_t)g->nranks)
+        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "%ux%u frame for %d row blocks", width, height, g->nranks);
+    const uint32_t old_w = g->width, old_h = g->height;
     g->width = width;
     g->height = height;
-    if (g->format && (uint64_t)width * height * pixel_bytes(g->format) > g->dst_bytes) {
+    for (LocalRank& lr : g->local) {
+        /* the row-block split of SURVEY.md §8(e) (wcpt_row_block): blocks differ by at most one row; frame size and
+         * block are set in one step, so no rank ever allocates more than its block (zeroed: CreateScreen) */
+        uint32_t y0 = 0, rows = 0;
+        block_of(g, lr.rank, y0, rows);
+        const int rc = wcpt::set_frame_block(lr.ctx, width, height, y0, rows);
+        if (rc) {
+            g->width = old_w;
+            g->height = old_h;
+            return rc;
+        }
+    }
+    if (g->format && g->root_local >= 0 && (uint64_t)width * height * pixel_bytes(g->format) > g->dst_bytes) {
         g->format = 0; /* the output no longer holds the frame: stop presenting until a new one is set */
         g->dst = g->dst_bytes = 0;
         const int rc = attach_payloads(g);
@@ -220,20 +471,24 @@ int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
 int wcpt_group_set_output(wcpt_group* g, int format, uint64_t dst, uint64_t bytes)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
-    if (dst == 0) {
+    if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
+    const bool holds_root = g->root_local >= 0;
+    if ((holds_root && dst == 0) || format == 0) {
         g->format = 0;
         g->dst = g->dst_bytes = 0;
         return attach_payloads(g);
     }
     if (!valid_format(format)) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "output format %d (3, 4 or 8)", format);
-    if ((dst & 3u) || (format == WCPT_PAYLOAD_RGBA32F && (dst & 15u)))
-        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "misaligned group output");
-    if (g->width && (uint64_t)g->width * g->height * pixel_bytes(format) > bytes)
-        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group output of %llu bytes < %ux%u x %llu",
-                           (unsigned long long)bytes, g->width, g->height, (unsigned long long)pixel_bytes(format));
+    if (holds_root) {
+        if ((dst & 3u) || (format == WCPT_PAYLOAD_RGBA32F && (dst & 15u)))
+            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "misaligned group output");
+        if (g->width && (uint64_t)g->width * g->height * pixel_bytes(format) > bytes)
+            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group output of %llu bytes < %ux%u x %llu",
+                               (unsigned long long)bytes, g->width, g->height, (unsigned long long)pixel_bytes(format));
+    }
     g->format = format;
-    g->dst = dst;
-    g->dst_bytes = bytes;
+    g->dst = holds_root ? dst : 0;
+    g->dst_bytes = holds_root ? bytes : 0;
     return attach_payloads(g);
 }
 
@@ -241,29 +496,103 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
                       const uint64_t* draw_commands)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
     if (!scene || !materials || !spheres || !draw_commands)
         return group_error(WCPT_ERROR_INVALID_ARGUMENT, "wcpt_group_render: null argument");
     if (!g->width) return group_error(WCPT_ERROR_NO_SCREEN, "wcpt_group_render: no screen (wcpt_group_create_screen)");
-    for (int r = 0; r < g->n; r++) {
-        const int rc = wcpt_render(g->ctx[r], scene, materials[r], spheres[r], draw_commands[r]);
+    const size_t nl = g->local.size();
+    const bool exchange = presenting(g) && g->nranks > 1;
+    const int b = g->overlap ? (int)(g->frames % kPayloadBuffers) : 0;
+    /* 1. every rank's arguments first: an argument error leaves every accumulation image as it was */
+    for (size_t i = 0; i < nl; i++) {
+        const int rc = wcpt::render_validate(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
         if (rc) return rc;
     }
-    if (!g->format || g->n == 1) return WCPT_SUCCESS; /* the root rendered its block into the output already */
-    const uint64_t px = pixel_bytes(g->format);
-    ncclResult_t e = ncclGroupStart();
-    if (e != ncclSuccess) return nccl_fail(e, "ncclGroupStart");
-    ncclResult_t first = ncclSuccess;
-    for (int r = 0; r < g->n && first == ncclSuccess; r++) {
-        if (r == g->root) continue;
-        const uint64_t bytes = (uint64_t)g->width * g->rows[r] * px;
-        void* at = reinterpret_cast<void*>(g->dst + (uint64_t)g->width * g->y0[r] * px);
-        first = ncclSend(g->payload[r], bytes, ncclUint8, g->root, g->comm[r], wcpt::context_stream(g->ctx[r]));
-        if (first == ncclSuccess)
-            first = ncclRecv(at, bytes, ncclUint8, r, g->comm[g->root], wcpt::context_stream(g->ctx[g->root]));
+    /* 2. point each sender's render at payload b; its previous reader must be done (device-side wait) */
+    if (exchange) {
+        for (LocalRank& lr : g->local) {
+            if (lr.rank == g->root) continue;
+            uint32_t y0 = 0, rows = 0;
+            block_of(g, lr.rank, y0, rows);
+            const uint64_t bytes = (uint64_t)g->width * rows * pixel_bytes(g->format);
+            if (!lr.payload[b] || lr.payload_cap[b] < bytes)
+                return group_error(WCPT_ERROR_INVALID_ARGUMENT, "rank %d: payload missing (set the output again)", lr.rank);
+            if (lr.sent_pending[b]) {
+                GHIP(hipSetDevice(lr.device), "hipSetDevice");
+                GHIP(hipStreamWaitEvent(wcpt::context_stream(lr.ctx), lr.sent[b], 0), "hipStreamWaitEvent(sent)");
+            }
+            const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[b]), bytes,
+                                                  (uint32_t)g->format);
+            if (rc) return rc;
+        }
     }
-    e = ncclGroupEnd();
-    if (first != ncclSuccess) return nccl_fail(first, "ncclSend/ncclRecv");
-    if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
+    /* 3. render every rank (validated: a failure now is a device/launch failure, and the ranks are out of step) */
+    for (size_t i = 0; i < nl; i++) {
+        const int rc = wcpt_render(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
+        if (rc) {
+            g->broken = true;
+            return rc;
+        }
+    }
+    g->frames++;
+    if (!exchange) return WCPT_SUCCESS; /* the root rendered its block into the output already */
+    /* 4. the gather: senders on their communication streams after their render (or in line), the root receiving */
+    const uint64_t px = pixel_bytes(g->format);
+    for (LocalRank& lr : g->local) {
+        GHIP(hipSetDevice(lr.device), "hipSetDevice");
+        const hipStream_t rs = wcpt::context_stream(lr.ctx);
+        GHIP(hipEventRecord(lr.ready[b], rs), "hipEventRecord(ready)");
+        if (g->overlap && lr.rank != g->root) GHIP(hipStreamWaitEvent(lr.comm_stream, lr.ready[b], 0), "hipStreamWaitEvent");
+    }
+    auto xfer_stream = [&](LocalRank& lr) { return g->overlap ? lr.comm_stream : wcpt::context_stream(lr.ctx); };
+    if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
+        LocalRank& rt = g->local[g->root_local]; /* the COPY transport is single-process: the root is local */
+        for (LocalRank& lr : g->local) {
+            if (lr.rank == g->root) continue;
+            uint32_t y0 = 0, rows = 0;
+            block_of(g, lr.rank, y0, rows);
+            void* at = reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
+            GHIP(hipSetDevice(lr.device), "hipSetDevice");
+            GHIP(hipMemcpyPeerAsync(at, rt.device, lr.payload[b], lr.device, (uint64_t)g->width * rows * px,
+                                    xfer_stream(lr)),
+                 "hipMemcpyPeerAsync(block)");
+        }
+    } else {
+        /* every argument was checked above, so no call below can fail on its arguments; a failure here is the
+         * transport's, and a half-posted exchange is aborted rather than launched */
+        ncclResult_t e = ncclGroupStart();
+        if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupStart"));
+        ncclResult_t first = ncclSuccess;
+        const char* what = "";
+        for (LocalRank& lr : g->local) {
+            if (first != ncclSuccess) break;
+            if (lr.rank != g->root) {
+                uint32_t y0 = 0, rows = 0;
+                block_of(g, lr.rank, y0, rows);
+                first = ncclSend(lr.payload[b], (uint64_t)g->width * rows * px, ncclUint8, g->root, lr.comm, xfer_stream(lr));
+                what = "ncclSend";
+                continue;
+            }
+            for (int r = 0; r < g->nranks && first == ncclSuccess; r++) {
+                if (r == g->root) continue;
+                uint32_t y0 = 0, rows = 0;
+                block_of(g, r, y0, rows);
+                void* at = reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
+                first = ncclRecv(at, (uint64_t)g->width * rows * px, ncclUint8, r, lr.comm,
+                                 g->overlap ? lr.comm_stream : wcpt::context_stream(lr.ctx));
+                what = "ncclRecv";
+            }
+        }
+        e = ncclGroupEnd();
+        if (first != ncclSuccess) return break_group(g, nccl_fail(first, what));
+        if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupEnd"));
+    }
+    for (LocalRank& lr : g->local) {
+        if (lr.rank == g->root) continue;
+        GHIP(hipSetDevice(lr.device), "hipSetDevice");
+        GHIP(hipEventRecord(lr.sent[b], xfer_stream(lr)), "hipEventRecord(sent)");
+        lr.sent_pending[b] = true;
+    }
     return WCPT_SUCCESS;
 }
 
@@ -271,10 +600,21 @@ int wcpt_group_sync(wcpt_group* g)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
     int first = WCPT_SUCCESS;
-    for (int r = 0; r < g->n; r++) {
-        const int rc = wcpt_sync(g->ctx[r]);
+    for (LocalRank& lr : g->local) {
+        int rc = wcpt_sync(lr.ctx);
+        if (!rc && lr.comm_stream) {
+            (void)hipSetDevice(lr.device);
+            const hipError_t e = hipStreamSynchronize(lr.comm_stream);
+            if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize(communication)");
+        }
+        if (!rc && lr.comm) {
+            ncclResult_t async = ncclSuccess;
+            if (ncclCommGetAsyncError(lr.comm, &async) == ncclSuccess && async != ncclSuccess)
+                rc = break_group(g, nccl_fail(async, "RCCL asynchronous error"));
+        }
         if (rc && !first) first = rc;
     }
+    if (!first && g->broken) first = group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
     return first;
 }
 

@@ -336,10 +336,12 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         const uint64_t nodes = bb ? (bb->bytes - o) / sizeof(wcpt_node) : ~0ull;
         uint64_t flags = (ctx->packed_refs && nodes < (1ull << 24) && dc[d].indexCount < (1u << 24)) ? 1u : 0u;
         if (dc[d].indexCount < (1u << 24)) flags |= 2u; /* pt_device.h kTriFlagIndex24 */
-        if (flags & 1u) {
-            /* pt_device.h kTriFlagSmallLeaves: scanned on the device once per BVH buffer generation */
+        /* pt_device.h kTriFlagSmallLeaves / kTriFlagLeafRecords: scanned on the device once per BVH buffer generation,
+         * which only the triangle cache tracks; with the cache off the BVH may change behind the runtime on any frame,
+         * and a scan per render would block the host, so the fast leaf layout is simply not used */
+        if ((flags & 1u) && ctx->tri_cache) {
             const uint64_t gb = bb->generation;
-            if (!(ctx->tri_cache && t.leaves_valid && t.bvh == dc[d].bvhBuffer && t.gen_bvh == gb && t.bvh_nodes == nodes &&
+            if (!(t.leaves_valid && t.bvh == dc[d].bvhBuffer && t.gen_bvh == gb && t.bvh_nodes == nodes &&
                   t.bvh_ntri == ntri)) {
                 if (!ctx->d_scan) HIP_TRY(ctx, hipMalloc(&ctx->d_scan, sizeof(uint32_t)), "hipMalloc(leaf scan flag)");
                 HIP_TRY(ctx, wcpt::launch_scan_leaf_counts(reinterpret_cast<const void*>(dc[d].bvhBuffer), (uint32_t)nodes,
@@ -437,11 +439,10 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
     return WCPT_SUCCESS;
 }
 
-int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
-                  uint64_t draws, int mode)
+/* The argument checks of wcpt_render that need no device work (render_common, wcpt::render_validate). */
+int check_render_args(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                      uint64_t draws, int mode)
 {
-    int rc = bind(ctx);
-    if (rc) return rc;
     if (!scene) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: null SceneData");
     if (!ctx->image || ctx->width == 0 || ctx->rows == 0)
         return set_error(ctx, WCPT_ERROR_NO_SCREEN, "wcpt_render: no output image (call wcpt_create_screen)");
@@ -451,6 +452,21 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: drawCommandCount > 0 with null draw commands");
     if (materials == 0 && (scene->sphereCount > 0 || scene->drawCommandCount > 0))
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: null material buffer");
+    if (ctx->wire && mode == wcpt::kModeRender &&
+        (uint64_t)ctx->width * ctx->rows * payload_pixel_bytes(ctx->wire_ch) > ctx->wire_bytes)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%u x %u B",
+                         (unsigned long long)ctx->wire_bytes, ctx->width, ctx->rows,
+                         (unsigned)payload_pixel_bytes(ctx->wire_ch));
+    return WCPT_SUCCESS;
+}
+
+int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                  uint64_t draws, int mode)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    rc = check_render_args(ctx, scene, materials, spheres, draws, mode);
+    if (rc) return rc;
     wcpt::LaunchArgs a;
     a.sd = *scene;
     a.materials = reinterpret_cast<const wcpt_material*>(materials);
@@ -459,13 +475,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.image = ctx->image;
     a.wire = nullptr;
     a.wire_ch = ctx->wire_ch;
-    if (ctx->wire && mode == wcpt::kModeRender) {
-        if ((uint64_t)ctx->width * ctx->rows * payload_pixel_bytes(ctx->wire_ch) > ctx->wire_bytes)
-            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%u x %u B",
-                             (unsigned long long)ctx->wire_bytes, ctx->width, ctx->rows,
-                             (unsigned)payload_pixel_bytes(ctx->wire_ch));
-        a.wire = ctx->wire;
-    }
+    if (ctx->wire && mode == wcpt::kModeRender) a.wire = ctx->wire;
     a.W = ctx->width;
     a.H = ctx->height;
     a.y0 = ctx->y0;
@@ -536,7 +546,65 @@ int read_status(wcpt_context* ctx)
  * through the same last-error strings as the C entry points. */
 namespace wcpt {
 hipStream_t context_stream(wcpt_context* ctx) { return ctx ? ctx->stream : nullptr; }
+int context_device(wcpt_context* ctx) { return ctx ? ctx->device : -1; }
 int context_error(wcpt_context* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
+
+/* Every check wcpt_render would make before it launches anything, with no launch: the argument checks and, per draw
+ * command, the index-count bound of the record build (prepare_tri_records). A group validates all its ranks first, so
+ * that an argument error cannot leave some ranks a frame ahead of the others. */
+int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
+                    uint64_t draws)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    rc = check_render_args(ctx, scene, materials, spheres, draws, kModeRender);
+    if (rc) return rc;
+    const uint32_t n = scene->drawCommandCount;
+    if (n == 0) return WCPT_SUCCESS;
+    std::vector<wcpt_draw_command> dc(n);
+    const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
+    uint64_t off = 0;
+    Buffer* db = buffer_at(ctx, draws, off);
+    if (ctx->tri_cache && db && shadow_known(*db, off, dbytes)) {
+        std::memcpy(dc.data(), db->shadow.data() + off, dbytes);
+    } else {
+        HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
+                                    ctx->stream), "hipMemcpyAsync(draw commands)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
+    }
+    for (uint32_t d = 0; d < n; d++) {
+        const uint32_t ntri = dc[d].indexCount / 3u;
+        uint64_t oi = 0;
+        Buffer* bi = buffer_at(ctx, dc[d].indexBuffer, oi);
+        if (bi && (uint64_t)ntri * 12ull > bi->bytes - oi)
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT,
+                             "draw command %u: indexCount %u exceeds its index buffer (%llu bytes from offset %llu)", d,
+                             dc[d].indexCount, (unsigned long long)(bi->bytes - oi), (unsigned long long)oi);
+        if (ntri && (dc[d].vertexBuffer == 0 || dc[d].indexBuffer == 0))
+            return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "draw command %u: null vertex/index buffer", d);
+    }
+    return WCPT_SUCCESS;
+}
+
+/* CreateScreen of one row block in one step: the frame's size and the context's block [y0, y0 + rows) are set
+ * together, so only the block is allocated (and zeroed), whatever the previous frame's size was. */
+int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows)
+{
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (width == 0 || rows == 0 || (uint64_t)y0 + rows > height)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "row block [%u,%u) of a %ux%u frame", y0, y0 + rows, width,
+                         height);
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    ctx->sharded = true;
+    rc = alloc_image(ctx, width, height, y0, rows);
+    if (rc) return rc;
+    if (!ctx->external_bytes) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->image, 0, (uint64_t)width * rows * 16ull, ctx->stream), "hipMemsetAsync(image)");
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    }
+    return WCPT_SUCCESS;
+}
 } // namespace wcpt
 
 extern "C" {

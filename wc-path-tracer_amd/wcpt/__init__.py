@@ -6,7 +6,7 @@ package is the Python host mirror used by tests and the benchmark.
 from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL,
                    KERNEL_WAVEFRONT, LIB_PATH, MATERIAL_DIELECTRIC, MATERIAL_DTYPE, MATERIAL_METAL, NODE_DTYPE,
                    SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, WcptError, lib)
-from .renderer import Context, DeviceScene, Editor, Group, PathTracingRenderer
+from .renderer import Context, DeviceScene, Editor, Group, PathTracingRenderer, group_unique_id
 from . import scene
 from . import _lib
 
@@ -14,7 +14,7 @@ __all__ = [
     "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
-    "PathTracingRenderer", "Editor", "Group", "scene", "device_count", "runtime_version",
+    "PathTracingRenderer", "Editor", "Group", "group_unique_id", "scene", "device_count", "runtime_version",
 ]
 
 

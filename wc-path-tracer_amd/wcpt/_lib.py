@@ -80,7 +80,12 @@ DIAG_FIELDS = ("wave_interior_steps", "lane_interior_steps", "wave_triangle_step
 # the reference's uint nodeStack[32] (pathTracer.comp:151): segments that write past it, and its deepest use (a max)
 REF_STACK_FIELDS = ("ref_stack_overflow_segments", "ref_stack_max")
 COUNTER_FIELDS = WORK_FIELDS + REF_STACK_FIELDS
-ABI_VERSION = 2
+# multi-device groups (wcpt_group_*)
+GROUP_TRANSPORT_RCCL = 0
+GROUP_TRANSPORT_COPY = 1
+GROUP_UNIQUE_ID_BYTES = 128
+GROUP_OPTION_OVERLAP = 1
+ABI_VERSION = 3
 assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
 assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
 
@@ -105,6 +110,15 @@ class Camera(C.Structure):
                 ("pitch", C.c_float), ("fov", C.c_float), ("projection", C.c_float * 16),
                 ("view", C.c_float * 16), ("inverseProjection", C.c_float * 16),
                 ("inverseView", C.c_float * 16)]
+
+
+class GroupInfo(C.Structure):
+    """wcpt_group_info (include/wcpt.h)."""
+    _fields_ = [(n, C.c_int32) for n in ("nranks", "local_ranks", "first_local_rank", "root", "transport", "overlap",
+                                         "distinct_devices", "broken")] + [("frames", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
 class SceneC(C.Structure):
@@ -167,6 +181,11 @@ _PROTOTYPES = {
     "wcpt_group_set_output": (_i, [_p, _i, _u64, _u64]),
     "wcpt_group_render": (_i, [_p, _p, C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]),
     "wcpt_group_sync": (_i, [_p]),
+    "wcpt_group_create_ex": (_i, [C.POINTER(_i), _i, _i, _i, C.POINTER(_p)]),
+    "wcpt_group_unique_id": (_i, [C.POINTER(C.c_uint8)]),
+    "wcpt_group_create_rank": (_i, [_i, _i, _i, _i, C.POINTER(C.c_uint8), C.POINTER(_p)]),
+    "wcpt_group_set_option": (_i, [_p, _i, _i]),
+    "wcpt_group_info_get": (_i, [_p, C.POINTER(GroupInfo)]),
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOTYPES)

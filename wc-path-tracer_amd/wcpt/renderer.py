@@ -11,8 +11,8 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, OPTION_DIAGNOSTICS, MATERIAL_DTYPE, SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera,
-                   Counters, WcptError, check, lib, ptr)
+from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, GROUP_TRANSPORT_RCCL, GROUP_UNIQUE_ID_BYTES, OPTION_DIAGNOSTICS,
+                   MATERIAL_DTYPE, SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, Counters, GroupInfo, WcptError, check, lib, ptr)
 from . import scene as _scene
 
 
@@ -211,18 +211,47 @@ class DeviceScene:
         self.buffers = []
 
 
-class Group:
-    """One frame on several devices from one host thread (include/wcpt.h wcpt_group_*): rank r renders
-    rows [r*H/N, (r+1)*H/N) on devices[r], and a set output gathers every frame's blocks to the root over RCCL."""
+def group_unique_id() -> bytes:
+    """wcpt_group_unique_id: the 128-byte RCCL id the root's process hands to every process of a rank group."""
+    buf = (C.c_uint8 * GROUP_UNIQUE_ID_BYTES)()
+    check(lib.wcpt_group_unique_id(buf))
+    return bytes(buf)
 
-    def __init__(self, devices, root: int = 0):
-        devs = (C.c_int * len(devices))(*devices)
+
+class Group:
+    """One frame on several devices (include/wcpt.h wcpt_group_*): rank r renders rows
+    [r*H/N, (r+1)*H/N) on its device, and a set output gathers every frame's blocks to the root.
+
+    ``Group(devices, root, transport)`` holds every rank in this process (one host thread, like the reference's
+    host); ``Group.rank(device, nranks, rank, root, uid)`` holds one rank of a one-process-per-device group. The
+    local ranks are ``self.ranks``; ``context(r)`` is rank r's context (None for a rank of another process)."""
+
+    def __init__(self, devices=None, root: int = 0, transport: int = GROUP_TRANSPORT_RCCL, _rank=None):
         h = C.c_void_p()
-        check(lib.wcpt_group_create(devs, len(devices), root, C.byref(h)))
+        if _rank is None:
+            devs = (C.c_int * len(devices))(*devices)
+            check(lib.wcpt_group_create_ex(devs, len(devices), root, transport, C.byref(h)))
+            self.ranks = list(range(len(devices)))
+            self.devices = list(devices)
+            self.nranks = len(devices)
+        else:
+            device, nranks, rank, uid = _rank
+            idp = None
+            if uid is not None:
+                assert len(uid) == GROUP_UNIQUE_ID_BYTES
+                idp = (C.c_uint8 * GROUP_UNIQUE_ID_BYTES).from_buffer_copy(uid)
+            check(lib.wcpt_group_create_rank(device, nranks, rank, root, idp, C.byref(h)))
+            self.ranks = [rank]
+            self.devices = [device]
+            self.nranks = nranks
         self.h = h
-        self.devices = list(devices)
         self.root = root
-        self.contexts = [Context.borrowed(lib.wcpt_group_context(h, r), d) for r, d in enumerate(devices)]
+        self._ctx = {r: Context.borrowed(lib.wcpt_group_context(h, r), d) for r, d in zip(self.ranks, self.devices)}
+        self.contexts = [self._ctx[r] for r in self.ranks]
+
+    @classmethod
+    def rank(cls, device: int, nranks: int, rank: int, root: int = 0, uid: bytes | None = None) -> "Group":
+        return cls(root=root, _rank=(device, nranks, rank, uid))
 
     def close(self):
         if self.h:
@@ -243,21 +272,30 @@ class Group:
         except Exception:
             pass
 
-    def context(self, rank: int) -> Context:
-        return self.contexts[rank]
+    def context(self, rank: int) -> Context | None:
+        return self._ctx.get(rank)
+
+    def set_option(self, option: int, value: int):
+        check(lib.wcpt_group_set_option(self.h, option, value))
+
+    def info(self) -> dict:
+        out = GroupInfo()
+        check(lib.wcpt_group_info_get(self.h, C.byref(out)))
+        return out.as_dict()
 
     def create_screen(self, width: int, height: int):
         from .dist import row_block
         check(lib.wcpt_group_create_screen(self.h, width, height))
         self.width, self.height = width, height
-        for r, c in enumerate(self.contexts):   # a rank's context holds only its row block
-            c.width, c.height = width, row_block(height, len(self.contexts), r)[1]
+        for r, c in self._ctx.items():   # a rank's context holds only its row block
+            c.width, c.height = width, row_block(height, self.nranks, r)[1]
 
     def set_output(self, fmt: int, dst: int, nbytes: int):
         check(lib.wcpt_group_set_output(self.h, fmt, dst, nbytes))
 
     def render(self, sd: np.ndarray, materials, spheres, draws):
-        n = len(self.devices)
+        """materials / spheres / draws: one device address per local rank, in rank order."""
+        n = len(self.ranks)
         sd = np.ascontiguousarray(sd, dtype=SCENE_DATA_DTYPE)
         arr = [(C.c_uint64 * n)(*[int(v) for v in a]) for a in (materials, spheres, draws)]
         check(lib.wcpt_group_render(self.h, ptr(sd), *arr))
@@ -400,4 +438,4 @@ class Editor:
         return used
 
 
-__all__ = ["Context", "DeviceScene", "Group", "PathTracingRenderer", "Editor", "COUNTER_FIELDS"]
+__all__ = ["Context", "DeviceScene", "Group", "group_unique_id", "PathTracingRenderer", "Editor", "COUNTER_FIELDS"]
