@@ -1,0 +1,172 @@
+"""bench.py's one-process-per-GPU mode (what the driver's torchrun scaling run executes) end to end on CPU: two
+processes with torchrun's environment run bench.main() against a stand-in for the wcpt device API, so the host plumbing
+-- rendezvous, the RCCL id handed from rank 0 to every rank, barriers, per-rank work and block times gathered to rank 0,
+the max-over-ranks time and the one JSON line -- is exercised without a GPU. The device side of the same calls is
+covered by tests/test_gpu_multi.py (the group itself) and can only run with RCCL on a multi-GPU node."""
+import json
+import multiprocessing as mproc
+import os
+import socket
+import sys
+import types
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+UID = bytes((7 * i) % 256 for i in range(128))
+
+
+def _fake_wcpt(rank, nranks, log):
+    """The slice of the wcpt package bench.py uses in its group modes, recording what it was asked to do."""
+    import wcpt._lib as L
+    from wcpt import scene as real_scene
+
+    class Ctx:
+        def __init__(self, rows):
+            self.rows, self.prof = rows, []
+
+        def set_kernel(self, k):
+            log.append(("kernel", k))
+
+        def set_option(self, o, v):
+            pass
+
+        def profile_begin(self):
+            self.prof = []
+
+        def profile_end(self):
+            return 0.1 * len(self.prof) * (1 + rank), len(self.prof)
+
+        def render_counters(self, sd, *a):
+            c = {k: 0 for k in L.COUNTER_FIELDS}
+            c.update(pixels=self.rows * 8, segments=self.rows * 8 * 3, interior_visits=5, triangle_tests=7)
+            return c
+
+        def readback(self, rows=None):
+            return np.zeros((rows or self.rows, 8, 4), np.float32)
+
+        def buffer_alloc(self, n):
+            log.append(("output", n))
+            return 1
+
+        def buffer_address(self, b):
+            return 4096
+
+        def buffer_free(self, b):
+            pass
+
+    class Group:
+        def __init__(self, ctx, r):
+            self.ctx, self.ranks, self.contexts, self.frames = ctx, [r], [ctx], 0
+
+        @classmethod
+        def rank(cls, device, n, r, root=0, uid=None):
+            assert (device, n, r, root) == (rank, nranks, rank, 0)
+            assert uid == UID, "the RCCL id must reach every rank unchanged"
+            log.append(("group", device, n, r))
+            return cls(Ctx(5 if r == 0 else 4), r)
+
+        def context(self, r):
+            return self.ctx if r in self.ranks else None
+
+        def set_option(self, o, v):
+            log.append(("overlap", v))
+
+        def create_screen(self, W, H):
+            log.append(("screen", W, H))
+
+        def set_output(self, fmt, dst, n):
+            log.append(("set_output", fmt, dst != 0))
+
+        def render(self, sd, m, s, d):
+            assert len(m) == len(s) == len(d) == 1
+            self.ctx.prof.append(1)
+            self.frames += 1
+
+        def sync(self):
+            pass
+
+        def info(self):
+            return {"nranks": nranks, "local_ranks": 1, "first_local_rank": rank, "root": 0, "transport": 0,
+                    "overlap": 1, "distinct_devices": 1, "broken": 0, "frames": self.frames}
+
+        def close(self):
+            log.append(("closed",))
+
+    class DeviceScene:
+        def __init__(self, ctx, scene):
+            pass
+
+        def addresses(self):
+            return 1, 2, 3
+
+        def free(self):
+            pass
+
+    m = types.ModuleType("wcpt")
+    m.__path__ = []
+    m._lib, m.scene, m.Group, m.DeviceScene = L, real_scene, Group, DeviceScene
+    m.group_unique_id = lambda: UID
+    m.runtime_version = lambda: 70226015
+    m.SCENE_DATA_DTYPE = L.SCENE_DATA_DTYPE
+    return m
+
+
+def _rank_main(rank, world, port, out_dir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "wc-path-tracer_amd")]
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port - 1))
+    import wcpt  # noqa: F401  (the real package: its scene module builds the Cornell box on the host)
+    import wcpt.rdzv  # noqa: F401  (the real rendezvous, which stays registered under its name)
+    log = []
+    sys.modules["wcpt"] = _fake_wcpt(rank, world, log)
+    import bench
+    out = open(os.path.join(out_dir, f"rank{rank}.out"), "w")
+    sys.stdout = out
+    bench.main(["--gpus", str(world), "--config", "c1", "--steps", "3", "--warmup", "2", "--settle-ms", "0",
+                "--no-cpu-baseline"])
+    out.close()
+    json.dump([list(x) for x in log], open(os.path.join(out_dir, f"rank{rank}.log"), "w"))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_one_process_per_gpu_plumbing(tmp_path, world):
+    ctx = mproc.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    lines = [ln for ln in open(tmp_path / "rank0.out").read().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    for r in range(1, world):
+        assert not open(tmp_path / f"rank{r}.out").read().strip()      # one JSON line, from rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["ranks"] == world and d["steps"] == 3
+    assert d["group"]["transport"] == "rccl" and d["group"]["rccl_ranks"] == world
+    assert d["group"]["kind"].startswith("one process per GPU")
+    assert "torch not imported" in d["hip_runtime"]
+    # per-rank render times gathered in rank order (the stand-in's rank r takes 0.1 * (1 + r) ms per render); the
+    # roofline's kernel time is the slowest rank's
+    assert d["per_rank_block_ms"] == [pytest.approx(0.1 * (1 + r)) for r in range(world)]
+    assert d["kernel_ms_avg"] == pytest.approx(0.1 * world)
+    # the work of all ranks: rank 0 holds 5 rows, the others 4 (stand-in), 24 segments per row, 3 timed frames
+    assert d["segments_per_frame"] == 24 * (5 + 4 * (world - 1))
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    logs = [json.load(open(tmp_path / f"rank{r}.log")) for r in range(world)]
+    for r, log in enumerate(logs):
+        assert ["group", r, world, r] in log and ["closed"] in log
+        assert ["set_output", 3, r == 0] in log                      # rgb payloads; only the root names a frame
+        assert (["output", 256 * 256 * 12] in log) == (r == 0)         # c1: 256x256, rgb 12 B/px, on the root
+        assert ["set_output", 0, False] in log                         # presenting off for the untimed re-render
