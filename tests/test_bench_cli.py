@@ -131,3 +131,26 @@ def test_rendezvous_from_env_uses_master_port_plus_one(monkeypatch):
     with pytest.raises(ValueError):
         Rendezvous(2, 2)
     assert isinstance(bench.parse_args([]), argparse.Namespace)
+
+
+def test_rendezvous_skips_a_busy_port_and_a_foreign_listener():
+    """The hub's first port is taken by an unrelated listener (which accepts and never answers): the hub binds the next
+    free port, clients skip the silent one after their handshake times out, and the exchange works."""
+    port = _free_port()
+    squat = socket.socket()
+    squat.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    squat.bind(("127.0.0.1", port))
+    squat.listen(8)
+    try:
+        ctx = mproc.get_context("spawn")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_rdzv_worker, args=(r, 2, port, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        got = dict(q.get(timeout=60)[:2] for _ in range(2))
+        for p in ps:
+            p.join(timeout=30)
+            assert p.exitcode == 0
+        assert got[0] == got[1] == bytes(range(128))
+    finally:
+        squat.close()

@@ -1104,6 +1104,29 @@ __device__ __forceinline__ DrawGeom draw_geom(const wcpt_draw_command* __restric
 #endif
 struct PeelCache { uint32_t tag; v2f t; };
 constexpr uint32_t kNoPeel = 0xFFFFFFFFu;
+/* Take the pair's triangles in reference order (2j, then 2j+1; each iff accepted with t < rec.t, strict):
+ * the winner is tagged with the record offset (+1 for the second). WCPT_PAIR_MERGE=1 picks the pair's own winner first
+ * (the second only when strictly nearer, as the reference's second `<` against the updated rec.t would) and compares
+ * that one with rec.t: the same winner, with one compare-select on rec.t's dependency chain per pair instead of two. */
+#ifndef WCPT_PAIR_MERGE
+#define WCPT_PAIR_MERGE 0
+#endif
+__device__ __forceinline__ void pair_take(const PairHit& ph, uint32_t off, float& rt, uint32_t& tag)
+{
+#if WCPT_PAIR_MERGE
+    const float c0 = ph.hit0 ? ph.t.x : __builtin_inff();
+    const float c1 = ph.hit1 ? ph.t.y : __builtin_inff();
+    const bool second = c1 < c0;
+    const float cb = second ? c1 : c0;
+    if (cb < rt) {
+        rt = cb;
+        tag = off + (second ? 1u : 0u);
+    }
+#else
+    if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
+    if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+#endif
+}
 template <bool COUNT, bool DIAG, bool UNIFORM, bool PRIM>
 __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_t k0, uint32_t kend, float& rt,
                                           uint32_t& prim, Counters& cnt, PeelCache& pc)
@@ -1178,9 +1201,8 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
                 }
 #endif
                 count_tri<COUNT, DIAG>(cnt);
-                if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = o; }
                 count_tri<COUNT, DIAG>(cnt);
-                if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = o + 1u; }
+                pair_take(ph, o, rt, tag);
             }
             off = offEnd;
         }
@@ -1198,9 +1220,8 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         }
 #endif
         count_tri<COUNT, DIAG>(cnt);
-        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; tag = off; }
         count_tri<COUNT, DIAG>(cnt);
-        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+        pair_take(ph, off, rt, tag);
     }
     if (tag != kNoTag) prim = 3u * (2u * (tag / kBytes) + (tag & 1u));
     if (k < kfull) k = kfull;

@@ -7,17 +7,24 @@ is one process (src/main.jai:185-194), so it has no counterpart; this is what le
 system HIP runtime libwcpt.so binds, as a Jai host would) run one process per GPU under torchrun without importing
 torch -- torch brings its own HIP runtime into the process.
 
-Transport: TCP on the host network. Rank 0 listens on (addr, port); ranks 1..N-1 connect (retrying until `timeout`)
-and announce their rank; messages are length-prefixed byte strings. Under torchrun, `from_env` takes MASTER_ADDR and
-MASTER_PORT + 1 (torchrun's own store holds MASTER_PORT), or WCPT_RDZV_PORT.
+Transport: TCP on the host network. Rank 0 listens on the first free port of [port, port + span); ranks 1..N-1 try
+those ports in turn (until `timeout`), and a connection counts only after a handshake: the client sends a magic word,
+a job token and its rank, the hub answers with its magic word. So a port taken by an unrelated program, or by another
+job's rendezvous, is skipped rather than hung on. Messages are length-prefixed byte strings. Under torchrun,
+`from_env` starts at MASTER_PORT + 1 (torchrun's own store holds MASTER_PORT), or at WCPT_RDZV_PORT, and derives the
+token from MASTER_PORT, WORLD_SIZE and TORCHELASTIC_RUN_ID.
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
 import socket
 import struct
 import time
+
+MAGIC_CLIENT = b"WCPTRDZ1"
+MAGIC_HUB = b"WCPTRDZA"
 
 
 class RendezvousError(RuntimeError):
@@ -46,49 +53,79 @@ def _recv(sock: socket.socket) -> bytes:
 class Rendezvous:
     """Rank `rank` of `world` host processes. Rank 0 is the hub."""
 
-    def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29600, timeout: float = 300.0):
+    def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29600, timeout: float = 300.0,
+                 token: bytes = b"", span: int = 32):
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"rank {rank} of {world}")
         self.rank, self.world = rank, world
         self.peers: dict[int, socket.socket] = {}
         self.hub: socket.socket | None = None
         self._server: socket.socket | None = None
+        self.port = None
         if world == 1:
             return
+        tok = hashlib.sha256(token).digest()[:16]
         deadline = time.monotonic() + timeout
         if rank == 0:
-            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            srv.bind((addr, port))
-            srv.listen(world)
-            srv.settimeout(max(0.1, deadline - time.monotonic()))
+            srv = None
+            for p in range(port, port + span):
+                s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+                try:
+                    s.bind((addr, p))
+                except OSError:
+                    s.close()
+                    continue
+                srv, self.port = s, p
+                break
+            if srv is None:
+                raise RendezvousError(f"rank 0: no free port in [{port}, {port + span}) on {addr}")
+            srv.listen(4 * world)
             self._server = srv
             while len(self.peers) < world - 1:
+                srv.settimeout(max(0.1, deadline - time.monotonic()))
                 try:
                     c, _ = srv.accept()
                 except socket.timeout:
                     raise RendezvousError(f"rank 0: {len(self.peers)} of {world - 1} peers connected before the "
                                           f"timeout") from None
+                try:
+                    c.settimeout(5.0)
+                    hello = _recv_exact(c, len(MAGIC_CLIENT) + len(tok) + 4)
+                except (OSError, RendezvousError):
+                    c.close()
+                    continue
+                r = struct.unpack("<I", hello[-4:])[0]
+                if hello[:len(MAGIC_CLIENT)] != MAGIC_CLIENT or hello[len(MAGIC_CLIENT):-4] != tok or \
+                        not 0 < r < world or r in self.peers:
+                    c.close()                          # another job, or not a rendezvous client at all
+                    continue
+                c.sendall(MAGIC_HUB)
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 c.settimeout(timeout)
-                (r,) = struct.unpack("<I", _recv_exact(c, 4))
-                if not 0 < r < world or r in self.peers:
-                    c.close()
-                    raise RendezvousError(f"rank 0: unexpected peer rank {r}")
                 self.peers[r] = c
         else:
-            while True:
-                try:
-                    c = socket.create_connection((addr, port), timeout=5.0)
-                    break
-                except OSError:
+            hello = MAGIC_CLIENT + tok + struct.pack("<I", rank)
+            while self.hub is None:
+                for p in range(port, port + span):
+                    try:
+                        c = socket.create_connection((addr, p), timeout=2.0)
+                    except OSError:
+                        continue
+                    try:
+                        c.settimeout(2.0)
+                        c.sendall(hello)
+                        if _recv_exact(c, len(MAGIC_HUB)) == MAGIC_HUB:
+                            c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                            c.settimeout(timeout)
+                            self.hub, self.port = c, p
+                            break
+                    except (OSError, RendezvousError):
+                        pass
+                    c.close()
+                if self.hub is None:
                     if time.monotonic() > deadline:
-                        raise RendezvousError(f"rank {rank}: no rendezvous at {addr}:{port}") from None
+                        raise RendezvousError(f"rank {rank}: no rendezvous hub on {addr}:[{port}, {port + span})")
                     time.sleep(0.05)
-            c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            c.settimeout(timeout)
-            c.sendall(struct.pack("<I", rank))
-            self.hub = c
 
     @classmethod
     def from_env(cls, timeout: float = 300.0) -> "Rendezvous":
@@ -97,8 +134,10 @@ class Rendezvous:
         rank = int(os.environ.get("RANK", "0"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-        port = int(os.environ.get("WCPT_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
-        return cls(rank, world, addr, port, timeout)
+        master = os.environ.get("MASTER_PORT", "29500")
+        port = int(os.environ.get("WCPT_RDZV_PORT", int(master) + 1))
+        token = f"{master}/{world}/{os.environ.get('TORCHELASTIC_RUN_ID', '')}".encode()
+        return cls(rank, world, addr, port, timeout, token=token)
 
     # -- collectives over small host messages ---------------------------------------------------------------
     def broadcast(self, data: bytes | None = None) -> bytes:
