@@ -78,13 +78,21 @@ def algorithmic_bytes(c: dict) -> int:
             + 60 * c["hits"] + 28 * c["draw_fetches"] + (164 + 32) * c["pixels"])
 
 
+STALE_PROFILES: list = []  # profiles refused because they were measured on another build (reported in the line)
+
+
 def _profile_json(path, args):
-    """A committed profile summary (profiles/*.json) when it was measured on this config, kernel and tree."""
+    """A committed profile summary (profiles/*.json) when it was measured on this config, kernel, camera and build: a
+    profile that records another build id (wcpt_build_id of the library it measured) is refused, not reused."""
     if not os.path.exists(path):
         return None
     try:
         pm = json.load(open(path))
     except (OSError, ValueError):
+        return None
+    build = getattr(args, "build_id", None)
+    if build is not None and pm.get("build_id") != build:
+        STALE_PROFILES.append(f"{os.path.basename(path)}: build {pm.get('build_id')} != loaded {build}")
         return None
     if (pm.get("config") == args.config and pm.get("kernel") == args.kernel and args.bvh == "midpoint" and
             getattr(args, "camera", "still") == pm.get("camera", "still")):
@@ -128,7 +136,7 @@ def roofline(args, tot, render_s, frame_s) -> dict:
                 "unit": "G wave64 VALU instructions/s", "frac": round(achieved / VALU_PEAK_GINSTR, 3),
                 "source": f"SQ_INSTS_VALU {valu:.4g}/render ({sq.get('source', 'profiles')}) over the live render "
                           f"time; peak {SIMDS} SIMDs x {CLOCK_GHZ} GHz / {CYCLES_PER_VALU} cycles"}
-        ceil = _valu_mix_ceiling(args.config)
+        ceil = _valu_mix_ceiling(args.config, getattr(args, "build_id", None))
         if ceil:
             # what this kernel's VALU mix can reach: each instruction class at the fastest rate measured for an
             # instruction of that class (tools/valu_peak.hip; v_add/v_mul/v_mov issue about twice as fast as v_fma)
@@ -152,7 +160,10 @@ def roofline(args, tot, render_s, frame_s) -> dict:
             head["reused_primary_lines_per_frame"] = int(reused / steps)
     else:
         head = {"bound": "unprofiled", "achieved": None, "peak": None, "unit": None, "frac": None,
-                "source": f"no SQ counter pass committed for {args.config} (profiles/sq_{args.config}.json)"}
+                "source": f"no SQ counter pass of this build committed for {args.config} "
+                          f"(profiles/sq_{args.config}.json)"}
+    if STALE_PROFILES:
+        head["stale_profiles_refused"] = sorted(set(STALE_PROFILES))
     if sq is not None:
         head["binding"] = {k: sq[k] for k in ("resource", "valu_issue_share", "wave_cycle_split", "l2_hit_rate",
                                               "lane_utilisation_valu") if k in sq}
@@ -167,13 +178,17 @@ def _json_field(name: str, key: str):
         return None
 
 
-def _valu_mix_ceiling(config: str):
+def _valu_mix_ceiling(config: str, build=None):
     """Mix-weighted VALU ceiling (G wave64 instructions/s) of the config's dominant kernel: 1 / sum(f_c / R_c) over the
     instruction classes c of profiles/valu_mix_<config>.json (fractions f_c of SQ_INSTS_VALU) with the class rates R_c
     of profiles/valu_ceiling.json."""
     try:
         rates = json.load(open(os.path.join(ROOT, "profiles", "valu_ceiling.json")))["class_gwave_instr_per_s"]
-        mix = json.load(open(os.path.join(ROOT, "profiles", f"valu_mix_{config}.json")))["class_fraction"]
+        mj = json.load(open(os.path.join(ROOT, "profiles", f"valu_mix_{config}.json")))
+        if build is not None and mj.get("build_id") != build:
+            STALE_PROFILES.append(f"valu_mix_{config}.json: build {mj.get('build_id')} != loaded {build}")
+            return None
+        mix = mj["class_fraction"]
         t = sum(f / float(rates[c]) for c, f in mix.items() if f > 0)
         return round(1.0 / t, 1) if t > 0 else None
     except (OSError, ValueError, KeyError, TypeError, ZeroDivisionError):
@@ -674,6 +689,7 @@ def main(argv=None):
     name, W, H, spp, bounces, desc = CONFIGS[args.config]
     if args.kernel < 0:
         args.kernel = DEFAULT_KERNEL[args.config]
+    args.build_id = wcpt.build_id()
     rank, nranks = topo["rank"], topo["nranks"]
     scene = wscene.generate(name, bvh=args.bvh)
     frames = FrameSource(scene, W, H, bounces, spp, args.camera, args.warmup + args.steps)
@@ -790,6 +806,7 @@ def main(argv=None):
                       if transport == "rccl" else None, "overlap": not args.no_overlap, "devices": topo["devices"]
                       if topo["mode"] == "group" else None},
             "hip_runtime": hip_runtime_label(topo["mode"]),
+            "build_id": args.build_id,
             "primary_mrays_per_s": round(prim_all / elapsed_max / 1e6, 3),
             "segments_per_frame": int(segs_all / args.steps),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),

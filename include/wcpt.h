@@ -227,6 +227,9 @@ typedef uint64_t wcpt_buffer;      /* 0 is never a valid handle */
 
 /* ---- library / context ---------------------------------------------------------------------------- */
 int         wcpt_abi_version(void);
+/* Identity of this build's sources and compile flags (a short hash): measurements recorded against one build (e.g. a
+ * counter profile) can tell whether they describe the library that is loaded. */
+const char* wcpt_build_id(void);
 int         wcpt_device_count(int* count);
 int         wcpt_create(int device, wcpt_context** out_ctx);
 int         wcpt_destroy(wcpt_context* ctx);                       /* Deinit, PathTracingRenderer.jai:473 */

@@ -109,6 +109,7 @@ def _fake_wcpt(rank, nranks, log):
     m._lib, m.scene, m.Group, m.DeviceScene = L, real_scene, Group, DeviceScene
     m.group_unique_id = lambda: UID
     m.runtime_version = lambda: 70226015
+    m.build_id = lambda: "stand-in"
     m.SCENE_DATA_DTYPE = L.SCENE_DATA_DTYPE
     return m
 

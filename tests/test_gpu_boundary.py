@@ -187,3 +187,68 @@ def test_buffer_range_checks_do_not_wrap(gpu_ctx):
         assert gpu_ctx.buffer_size(b) == 64             # no grow to a wrapped size
     finally:
         gpu_ctx.buffer_free(b)
+
+
+def _fat_leaf_bvh(nodes, min_tris=90, max_tris=600):
+    """The same BVH with one interior node turned into a leaf over its whole (contiguous) subtree: a valid tree for
+    the same triangles whose new leaf holds >= 255 index positions, outside what the wavefront's fast leaf layout was
+    scanned for."""
+    def span(i):
+        n = nodes[i]
+        if n["triangleCount"]:
+            return int(n["leftNodeOrTriangleIndex"]), int(n["leftNodeOrTriangleIndex"] + n["triangleCount"])
+        a0, a1 = span(int(n["leftNodeOrTriangleIndex"]))
+        b0, b1 = span(int(n["leftNodeOrTriangleIndex"]) + 1)
+        assert a1 == b0 or b1 == a0
+        return min(a0, b0), max(a1, b1)
+    for i in range(1, len(nodes)):
+        n = nodes[i]
+        if n["triangleCount"]:
+            continue
+        lo, hi = span(i)
+        if min_tris * 3 <= hi - lo <= max_tris * 3:
+            out = nodes.copy()
+            out[i]["leftNodeOrTriangleIndex"] = lo
+            out[i]["triangleCount"] = hi - lo
+            return out, i
+    raise AssertionError("no subtree of the wanted size")
+
+
+def test_bvh_rewritten_behind_the_triangle_cache_stays_in_bounds(gpu_ctx):
+    """the wavefront's fast leaf layout is chosen from a scan of the draw's BVH that the triangle cache
+    keeps per buffer generation. A BVH rewritten by hipMemcpy (not wcpt_buffer_upload) with the cache on keeps the
+    stale layout: the frame may be wrong (a leaf of >= 255 index positions no longer fits a stack entry), but every
+    record load is bounded by the draw's records, so the render completes and reports no error. With the cache off,
+    or after the same bytes go through wcpt_buffer_upload, the frame is the oracle's for the rewritten tree."""
+    s = get_scene("atrium")
+    W, H = 48, 27
+    fat, node = _fat_leaf_bvh(s.meshes[0].nodes)
+    assert fat[node]["triangleCount"] >= 255
+    rewritten = _with_mesh(s, wscene.HostBVH(s.meshes[0].positions, s.meshes[0].indices, fat))
+    ref, _ = oracle.render_scene(rewritten, W, H, max_bounce=4, threads=8)
+    gpu_ctx.set_kernel(wcpt.KERNEL_WAVEFRONT)
+    dev = wcpt.DeviceScene(gpu_ctx, s)
+    try:
+        gpu_ctx.create_screen(W, H)
+        sd = s.scene_data(W, H, max_bounce=4)
+        gpu_ctx.render(sd, *dev.addresses())            # the scan learns the original tree: fast layout
+        gpu_ctx.sync()
+        bvh_addr = gpu_ctx.buffer_address(dev.buffers[4])  # materials, spheres, vertices, indices, BVH, draws
+        _device_write(bvh_addr, fat)                     # behind the cache
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()                                   # completes; no stack or memory fault
+        stale = gpu_ctx.readback(H)
+        assert np.isfinite(stale).all()
+        gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 0)
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()
+        assert_close(gpu_ctx.readback(H), ref)
+        gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 1)
+        gpu_ctx.buffer_upload(dev.buffers[4], fat)      # through the runtime: re-scanned, the general layout
+        gpu_ctx.render(sd, *dev.addresses())
+        gpu_ctx.sync()
+        assert_close(gpu_ctx.readback(H), ref)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 1)
+        gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        dev.free()

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--kernel", default="pt_megakernel<false")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--build-id", default=None, help="wcpt_build_id() of the library the passes measured")
     ap.add_argument("--config", default=None)
     ap.add_argument("--kernel-id", type=int, default=0)
     ap.add_argument("--per-frame", type=int, default=2,
@@ -76,6 +77,8 @@ def main():
         d["config"] = a.config
         d["kernel"] = a.kernel_id
     d["kernel_name_filter"] = a.kernel
+    if a.build_id:
+        d["build_id"] = a.build_id
     print(json.dumps(d, indent=1))
     if a.json:
         json.dump(d, open(a.json, "w"), indent=1)

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--cycles-per-sec", type=float, default=2.4e9)
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--build-id", default=None, help="wcpt_build_id() of the library the passes measured")
     ap.add_argument("--config", default=None, help="bench config the passes ran (bench.py reads sq_<config>.json)")
     ap.add_argument("--kernel-id", type=int, default=None, help="wcpt kernel variant (0 megakernel, 2 wavefront)")
     ap.add_argument("--bound", default=None, choices=["valu_issue", "memory_latency"],
@@ -57,6 +58,8 @@ def main():
     if a.kernel_id is not None:
         out["kernel_name_filter"] = out["kernel"]
         out["kernel"] = a.kernel_id
+    if a.build_id:
+        out["build_id"] = a.build_id
     print(json.dumps(out, indent=1))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)

@@ -611,6 +611,11 @@ extern "C" {
 
 int wcpt_abi_version(void) { return WCPT_ABI_VERSION; }
 
+#ifndef WCPT_BUILD_ID
+#define WCPT_BUILD_ID "unknown"
+#endif
+const char* wcpt_build_id(void) { return WCPT_BUILD_ID; }
+
 int wcpt_runtime_version(int* version)
 {
     if (!version) return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "null version");

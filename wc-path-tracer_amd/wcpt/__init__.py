@@ -14,7 +14,7 @@ __all__ = [
     "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
-    "PathTracingRenderer", "Editor", "Group", "group_unique_id", "scene", "device_count", "runtime_version",
+    "PathTracingRenderer", "Editor", "Group", "group_unique_id", "scene", "device_count", "runtime_version", "build_id",
 ]
 
 
@@ -23,6 +23,11 @@ def device_count() -> int:
     n = C.c_int()
     lib.wcpt_device_count(C.byref(n))
     return n.value
+
+
+def build_id() -> str:
+    """wcpt_build_id: hash of the library's sources and compile flags (profiles record the build they measured)."""
+    return lib.wcpt_build_id().decode()
 
 
 def runtime_version() -> int:

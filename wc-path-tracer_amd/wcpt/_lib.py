@@ -133,6 +133,7 @@ _i = C.c_int
 
 _PROTOTYPES = {
     "wcpt_abi_version": (_i, []),
+    "wcpt_build_id": (C.c_char_p, []),
     "wcpt_device_count": (_i, [C.POINTER(_i)]),
     "wcpt_create": (_i, [_i, C.POINTER(_p)]),
     "wcpt_destroy": (_i, [_p]),
