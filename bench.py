@@ -751,7 +751,7 @@ def main(argv=None):
         tot["reused_primary_segments"] = (spp - 1) * cp["segments"] * args.steps
     per_rank = [{"rank": int(r), "block_ms": round(ms / max(1, n), 4), "launches": int(n)}
                 for r, (ms, n) in zip(drv.ranks, prof)]
-    mine = {"elapsed": elapsed, "tot": tot, "per_rank": per_rank,
+    mine = {"elapsed": elapsed, "tot": tot, "per_rank": per_rank, "devices": [int(c.device) for c in drv.ctxs],
             "kernel_ms": sum(ms for ms, _ in prof), "launches": sum(n for _, n in prof)}
     allr = coll.gather_obj(json.loads(json.dumps(mine, default=int)))
 
@@ -772,7 +772,7 @@ def main(argv=None):
         segs_all, prim_all = float(T["segments"]), float(T["pixels"] * spp)
         value = segs_all / elapsed_max / 1e6
         info = drv.info()
-        distinct = info["distinct_devices"] if topo["mode"] == "group" else nranks
+        distinct = len({dv for a in allr for dv in a["devices"]})  # GPUs the ranks ran on (a rehearsal repeats one)
         kind = {"group": "one process, one host thread, all ranks (wcpt_group_create_ex)",
                 "ranks": "one process per GPU (wcpt_group_create_rank, ncclCommInitRank; host rendezvous wcpt.rdzv)",
                 "torch": f"one process per GPU, torch.distributed {args.dist_backend} gather (rehearsal path)"}

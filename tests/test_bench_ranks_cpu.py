@@ -24,7 +24,7 @@ def _fake_wcpt(rank, nranks, log):
 
     class Ctx:
         def __init__(self, rows):
-            self.rows, self.prof = rows, []
+            self.rows, self.prof, self.device = rows, [], rank
 
         def set_kernel(self, k):
             log.append(("kernel", k))

@@ -1,0 +1,89 @@
+"""Turn a tools/gpu_r04_sq.sh session (gpurun_out/<tag>) into the profile summaries bench.py prices its roofline from:
+profiles/sq_<cfg>.json, valu_mix_<cfg>.json, pmc_traffic_<cfg>.json, each stamped with the build id the session
+measured (bench.py refuses a profile of another build) and the kernel time from the session's own kernel stats.
+
+    python tools/r04_summaries.py gpurun_out/r04_sq [--configs c2 ref c3 c4] [--out profiles] [--source "round 4 ..."]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# per config: (kernel id, dominant-kernel filter, launches of it per frame, bound, resource, whole-frame PMC filters)
+SPEC = {
+    "c2": (0, "pt_megakernel<false", 1.0, "valu_issue",
+           "VALU issue (SQ_INSTS_VALU x 2 cycles over the SIMD cycles of the launch; the mix-weighted ceiling in "
+           "profiles/valu_mix_c2.json)", None),
+    "ref": (0, "pt_megakernel<false", 1.0, "valu_issue",
+            "VALU issue, with lane utilisation ~0.55: divergent waves (camera inside the mushroom, leaves of 1-43 "
+            "triangles)", None),
+    "c3": (2, "wf_trace<false", 1.0, "memory_latency",
+           "latency of dependent node fetches (waves parked on memory, SQ_WAIT_ANY share of wave cycles) and the loop "
+           "control between them", "wf_trace<false,wf_shade<false,wf_init<false"),
+    "c4": (2, "wf_trace<false", 130.0, "memory_latency",
+           "latency of dependent node fetches (waves parked on memory, SQ_WAIT_ANY share of wave cycles) and the loop "
+           "control between them", "wf_trace<false,wf_shade<false,wf_init<false"),
+}
+MIX = ("ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "INT32", "INT64", "CVT")
+
+
+def kernel_ms(d, cfg, filt):
+    for f in glob.glob(os.path.join(d, f"prof_{cfg}", "**", "*kernel_stats.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if filt in row["Name"]:
+                return float(row["AverageNs"]) / 1e6
+    raise SystemExit(f"{cfg}: no {filt} in the kernel stats")
+
+
+def counters(d, cfg, filt):
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(d, f"sq_{cfg}", "p*", "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if filt in row.get("Kernel_Name", ""):
+                per[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--configs", nargs="+", default=["c2", "ref", "c3", "c4"])
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles"))
+    ap.add_argument("--source", default=None)
+    a = ap.parse_args()
+    build = open(os.path.join(a.dir, "build_id")).read().strip()
+    tag = os.path.basename(os.path.normpath(a.dir))
+    for cfg in a.configs:
+        kid, filt, lpf, bound, resource, frame_filters = SPEC[cfg]
+        ms = kernel_ms(a.dir, cfg, filt)
+        src = (a.source or f"round 4 {tag}") + f" (tools/gpu_r04_sq.sh; {filt.split('<')[0]} {ms:.4f} ms avg from " \
+                                                 f"the session's kernel stats)"
+        py = sys.executable
+        subprocess.run([py, os.path.join(ROOT, "tools", "sq_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--kernel",
+                        filt, "--ms", str(ms), "--launches-per-frame", str(lpf), "--config", cfg, "--kernel-id",
+                        str(kid), "--bound", bound, "--resource", resource, "--source", src, "--build-id", build,
+                        "--json", os.path.join(a.out, f"sq_{cfg}.json")], check=True, stdout=subprocess.DEVNULL)
+        pm = [py, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--config", cfg,
+              "--kernel-id", str(kid), "--build-id", build, "--json", os.path.join(a.out, f"pmc_traffic_{cfg}.json")]
+        pm += ["--kernel", frame_filters, "--frame-kernel", "wf_init<false"] if frame_filters else ["--kernel", filt]
+        subprocess.run(pm, check=True, stdout=subprocess.DEVNULL)
+        m, n = counters(a.dir, cfg, filt)
+        tot = m.get("SQ_INSTS_VALU")
+        frac = {c: m[f"SQ_INSTS_VALU_{c}"] / tot for c in MIX if f"SQ_INSTS_VALU_{c}" in m}
+        frac["other"] = 1.0 - sum(frac.values())
+        json.dump({"config": cfg, "kernel": kid, "kernel_name_filter": filt, "dispatches": n.get("SQ_INSTS_VALU_ADD_F32"),
+                   "SQ_INSTS_VALU_per_launch": tot, "class_fraction": {k: round(v, 4) for k, v in frac.items()},
+                   "build_id": build,
+                   "source": src + "; one --pmc pass of SQ_INSTS_VALU and its classes; other = the remainder (moves, "
+                                   "selects, compares, min/max, bit ops)"},
+                  open(os.path.join(a.out, f"valu_mix_{cfg}.json"), "w"), indent=1)
+        print(f"{cfg}: build {build}, {filt} {ms:.4f} ms, summaries written")
+
+
+if __name__ == "__main__":
+    main()
