@@ -42,7 +42,13 @@ def main():
     per = load(a.dir)
     out = {}
     if a.frame_kernel:
-        frames = sum(len(next(iter(c.values()))) for n, c in per.items() if a.frame_kernel in n) // a.per_frame
+        # frames per counter: each counter comes from its own --pmc pass (a separate run, whose untimed settle phase
+        # renders its own number of frames), so every counter is divided by the frames of the pass that collected it
+        frames = defaultdict(int)
+        for n, c in per.items():
+            if a.frame_kernel in n:
+                for ctr, vals in c.items():
+                    frames[ctr] += len(vals)
         if not frames:
             raise SystemExit(f"no dispatches of {a.frame_kernel} in {a.dir}")
         filters = a.kernel.split(",")
@@ -50,7 +56,7 @@ def main():
             if not any(f in name for f in filters):
                 continue
             for c, vals in ctrs.items():
-                out[c] = out.get(c, 0.0) + sum(vals) / frames
+                out[c] = out.get(c, 0.0) + sum(vals) / (frames[c] / a.per_frame)
         if not out:
             raise SystemExit(f"no dispatches of {a.kernel} in {a.dir}")
     else:
