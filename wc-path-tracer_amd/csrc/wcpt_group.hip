@@ -23,9 +23,11 @@
  * sends, and an event marks the send's end; the render of frame k + 2, which rewrites that buffer, waits for that
  * event on the device (hipStreamWaitEvent), so the host never blocks. The root renders its block straight into the
  * presented frame and receives the others' rows on its communication stream, so its next render does not wait for the
- * slowest rank's transfer. Payload buffers come from the stream-ordered allocator (hipMallocAsync on the render
- * stream); a regrown buffer is released with hipFreeAsync on the communication stream after the last work that can
- * touch it, so a resize never synchronises the device.
+ * slowest rank's transfer. A payload buffer that must grow (a resize, a wider format) is replaced by a new hipMalloc
+ * buffer and the old one is retired: queued transfers may still read it, so it is freed at the next point where the
+ * group waits for all its work anyway (wcpt_group_sync, wcpt_group_destroy) -- a resize never synchronises the device
+ * (hipFree would). Plain device allocations, not the stream-ordered pool: they are what RCCL's transports expect of a
+ * user buffer.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -57,7 +59,7 @@ struct LocalRank {
     hipEvent_t ready[kPayloadBuffers] = {};  /* the render that wrote payload[b] has finished */
     hipEvent_t sent[kPayloadBuffers] = {};   /* the transfer that read payload[b] has finished */
     bool sent_pending[kPayloadBuffers] = {};
-    hipEvent_t fence = nullptr;              /* scratch: orders a stream-ordered free after the render stream */
+    std::vector<void*> retired;              /* replaced payload buffers, freed at the next group-wide wait */
 };
 
 } // namespace
@@ -120,22 +122,26 @@ void block_of(const wcpt_group* g, int rank, uint32_t& y0, uint32_t& rows)
 
 bool presenting(const wcpt_group* g) { return g->format != 0 && g->width != 0; }
 
-/* Release a payload buffer once every queued use of it is over: the render stream's work (a render writing it) is
- * fenced into the communication stream, and the free follows the transfers there. */
-int release_payload(LocalRank& lr, int b)
+/* Retire a payload buffer: queued renders and transfers may still touch it, so it is freed at the next group-wide wait
+ * (free_retired). */
+void release_payload(LocalRank& lr, int b)
 {
-    if (!lr.payload[b]) return WCPT_SUCCESS;
-    GHIP(hipSetDevice(lr.device), "hipSetDevice");
-    GHIP(hipEventRecord(lr.fence, wcpt::context_stream(lr.ctx)), "hipEventRecord(fence)");
-    GHIP(hipStreamWaitEvent(lr.comm_stream, lr.fence, 0), "hipStreamWaitEvent(fence)");
-    GHIP(hipFreeAsync(lr.payload[b], lr.comm_stream), "hipFreeAsync(payload)");
+    if (lr.payload[b]) lr.retired.push_back(lr.payload[b]);
     lr.payload[b] = nullptr;
     lr.payload_cap[b] = 0;
     lr.sent_pending[b] = false;
-    return WCPT_SUCCESS;
 }
 
-/* Size every sending rank's payload buffers for the current frame and format (stream-ordered: no device sync) and
+/* Free a rank's retired payloads; its render and communication streams have drained. */
+void free_retired(LocalRank& lr)
+{
+    if (lr.retired.empty()) return;
+    (void)hipSetDevice(lr.device);
+    for (void* p : lr.retired) (void)hipFree(p);
+    lr.retired.clear();
+}
+
+/* Size every sending rank's payload buffers for the current frame and format (replaced ones are retired: no device sync) and
  * point the root's render at its block of the presented frame. Called after a screen or output change. */
 int attach_payloads(wcpt_group* g)
 {
@@ -157,14 +163,12 @@ int attach_payloads(wcpt_group* g)
         GHIP(hipSetDevice(lr.device), "hipSetDevice");
         for (int b = 0; b < kPayloadBuffers; b++) {
             if (lr.payload_cap[b] >= bytes) continue;
-            int rc = release_payload(lr, b);
-            if (rc) return rc;
-            GHIP(hipSetDevice(lr.device), "hipSetDevice");
-            const hipError_t e = hipMallocAsync(&lr.payload[b], bytes, wcpt::context_stream(lr.ctx));
+            release_payload(lr, b);
+            const hipError_t e = hipMalloc(&lr.payload[b], bytes);
             if (e != hipSuccess) {
                 lr.payload[b] = nullptr;
                 (void)hipGetLastError();
-                return group_error(WCPT_ERROR_OUT_OF_DEVICE_MEMORY, "hipMallocAsync(payload of rank %d, %llu bytes): %s",
+                return group_error(WCPT_ERROR_OUT_OF_DEVICE_MEMORY, "hipMalloc(payload of rank %d, %llu bytes): %s",
                                    lr.rank, (unsigned long long)bytes, hipGetErrorString(e));
             }
             lr.payload_cap[b] = bytes;
@@ -186,7 +190,6 @@ int init_local(LocalRank& lr)
         GHIP(hipEventCreateWithFlags(&lr.ready[b], hipEventDisableTiming), "hipEventCreate");
         GHIP(hipEventCreateWithFlags(&lr.sent[b], hipEventDisableTiming), "hipEventCreate");
     }
-    GHIP(hipEventCreateWithFlags(&lr.fence, hipEventDisableTiming), "hipEventCreate");
     return WCPT_SUCCESS;
 }
 
@@ -364,11 +367,11 @@ int wcpt_group_destroy(wcpt_group* g)
     for (LocalRank& lr : g->local) {
         (void)hipSetDevice(lr.device);
         for (int b = 0; b < kPayloadBuffers; b++) {
-            if (lr.payload[b] && lr.comm_stream) (void)hipFreeAsync(lr.payload[b], lr.comm_stream);
+            if (lr.payload[b]) (void)hipFree(lr.payload[b]);
             if (lr.ready[b]) (void)hipEventDestroy(lr.ready[b]);
             if (lr.sent[b]) (void)hipEventDestroy(lr.sent[b]);
         }
-        if (lr.fence) (void)hipEventDestroy(lr.fence);
+        free_retired(lr);
         if (lr.comm_stream) {
             (void)hipStreamSynchronize(lr.comm_stream);
             (void)hipStreamDestroy(lr.comm_stream);
@@ -607,6 +610,7 @@ int wcpt_group_sync(wcpt_group* g)
             const hipError_t e = hipStreamSynchronize(lr.comm_stream);
             if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize(communication)");
         }
+        if (!rc) free_retired(lr);
         if (!rc && lr.comm) {
             ncclResult_t async = ncclSuccess;
             if (ncclCommGetAsyncError(lr.comm, &async) == ncclSuccess && async != ncclSuccess)
