@@ -445,9 +445,17 @@ class GroupBench:
             else:
                 self.g.set_output(self.fmt, 0, 0)
         self.addr = [list(a) for a in zip(*[d.addresses() for d in self.devs])]
+        # the per-rank address arrays, built once: a step's host work is one ctypes call (at 8 ranks a c2 block renders
+        # in ~0.07 ms, so the host's per-step cost has to stay well below that)
+        import ctypes as C
+        n = len(self.ranks)
+        self._arrs = [(C.c_uint64 * n)(*[int(v) for v in a]) for a in self.addr]
+        self._render = wcpt.lib.wcpt_group_render
 
     def render(self, sd):
-        self.g.render(sd, *self.addr)
+        rc = self._render(self.g.h, sd.ctypes.data, *self._arrs)
+        if rc:
+            wcpt._lib.check(rc)
 
     def sync(self):
         self.g.sync()

@@ -59,6 +59,7 @@ def _fake_wcpt(rank, nranks, log):
     class Group:
         def __init__(self, ctx, r):
             self.ctx, self.ranks, self.contexts, self.frames = ctx, [r], [ctx], 0
+            self.h = self
 
         @classmethod
         def rank(cls, device, n, r, root=0, uid=None):
@@ -83,6 +84,7 @@ def _fake_wcpt(rank, nranks, log):
             assert len(m) == len(s) == len(d) == 1
             self.ctx.prof.append(1)
             self.frames += 1
+            return 0
 
         def sync(self):
             pass
@@ -110,6 +112,8 @@ def _fake_wcpt(rank, nranks, log):
     m.group_unique_id = lambda: UID
     m.runtime_version = lambda: 70226015
     m.build_id = lambda: "stand-in"
+    # bench.py calls wcpt_group_render through the library with prebuilt arrays: route it to the stand-in group
+    m.lib = types.SimpleNamespace(wcpt_group_render=lambda h, sd, mm, ss, dd: h.render(sd, list(mm), list(ss), list(dd)))
     m.SCENE_DATA_DTYPE = L.SCENE_DATA_DTYPE
     return m
 
