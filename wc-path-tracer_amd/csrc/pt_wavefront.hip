@@ -534,6 +534,27 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
 }
 
 /* ---- shade ------------------------------------------------------------------------------------------ */
+#ifndef WCPT_SHADE_PREFETCH
+#define WCPT_SHADE_PREFETCH 1
+#endif
+/* One input queue slot of wf_shade: pixel, ray, light, transmittance and the trace's Intersect record. */
+struct PathIn {
+    uint32_t pix;
+    float4 r0, r1, li, tr, hi;
+};
+__device__ __forceinline__ PathIn load_path_in(const WfBuffers& b, uint32_t w, uint32_t n)
+{
+    PathIn q = {};
+    if (w < n) {
+        q.pix = b.in.pix[w];
+        q.r0 = b.in.ray0[w];
+        q.r1 = b.in.ray1[w];
+        q.li = b.in.light[w];
+        q.tr = b.in.trans[w];
+        q.hi = b.hit[w];
+    }
+    return q;
+}
 template <bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd, const wcpt_material* __restrict__ mats,
                                                         const wcpt_sphere* __restrict__ spheres,
@@ -546,16 +567,29 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.head = 0; /* the trace of this iteration has finished */
     const uint32_t n = *b.count_in;
     Counters cnt = {};
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+#if WCPT_SHADE_PREFETCH
+    /* The path state of the thread's next queue slot is loaded before the current one is shaded: the streams (path
+     * state in queue order, coalesced) have one iteration of the grid-stride loop to arrive instead of stalling its
+     * start, and the dependent gathers of the current path (normal, material) overlap them. */
+    PathIn nxt = load_path_in(b, blockIdx.x * blockDim.x + threadIdx.x, n);
+#endif
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
         const uint32_t w = base + threadIdx.x;
         bool cont = false;
         uint32_t p = 0, sample = 0, seed = 0, prim0 = kNoPrim;
         float rt0 = kInfinity;
         PathState ps;
+#if WCPT_SHADE_PREFETCH
+        const PathIn cur = nxt;
+        nxt = load_path_in(b, w + stride, n);
+#else
+        const PathIn cur = load_path_in(b, w, n);
+#endif
         if (w < n) {
-            p = b.in.pix[w];                     /* slot w of the compacted input queue */
-            const float4 r0 = b.in.ray0[w], r1 = b.in.ray1[w], li = b.in.light[w], tr = b.in.trans[w];
-            const float4 hi = b.hit[w];
+            p = cur.pix;                         /* slot w of the compacted input queue */
+            const float4 r0 = cur.r0, r1 = cur.r1, li = cur.li, tr = cur.tr;
+            const float4 hi = cur.hi;
             ps.ray.origin = mk3(r0.x, r0.y, r0.z);
             ps.ray.direction = mk3(r0.w, r1.x, r1.y);
             ps.totalLight = mk3(li.x, li.y, li.z);

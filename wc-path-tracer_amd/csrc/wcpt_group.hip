@@ -181,11 +181,14 @@ int attach_payloads(wcpt_group* g)
     return WCPT_SUCCESS;
 }
 
-/* Set up everything a local rank needs beyond its context (created by the caller). */
-int init_local(LocalRank& lr)
+/* Set up everything a local rank needs beyond its context (created by the caller). A group of one has no exchange and
+ * gets no communication stream: its device keeps exactly the context's streams (the wavefront pipelines' streams sit
+ * close to the device's hardware-queue limit). */
+int init_local(LocalRank& lr, int nranks)
 {
     GHIP(hipSetDevice(lr.device), "hipSetDevice");
-    GHIP(hipStreamCreateWithFlags(&lr.comm_stream, hipStreamNonBlocking), "hipStreamCreate(communication)");
+    if (nranks > 1)
+        GHIP(hipStreamCreateWithFlags(&lr.comm_stream, hipStreamNonBlocking), "hipStreamCreate(communication)");
     for (int b = 0; b < kPayloadBuffers; b++) {
         GHIP(hipEventCreateWithFlags(&lr.ready[b], hipEventDisableTiming), "hipEventCreate");
         GHIP(hipEventCreateWithFlags(&lr.sent[b], hipEventDisableTiming), "hipEventCreate");
@@ -260,7 +263,7 @@ int wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcp
         lr.rank = r;
         lr.device = devices[r];
         rc = wcpt_create(devices[r], &lr.ctx);
-        if (!rc) rc = init_local(lr);
+        if (!rc) rc = init_local(lr, n);
         if (rc) {
             wcpt_group_destroy(g);
             return rc;
@@ -332,7 +335,7 @@ int wcpt_group_create_rank(int device, int nranks, int rank, int root, const uin
     lr.rank = rank;
     lr.device = device;
     rc = wcpt_create(device, &lr.ctx);
-    if (!rc) rc = init_local(lr);
+    if (!rc) rc = init_local(lr, nranks);
     if (rc) {
         wcpt_group_destroy(g);
         return rc;
