@@ -339,8 +339,10 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          the render streams, in line with the renders.
  *   wcpt_group_sync        waits for every local rank's renders and transfers (and reports a traversal-stack
  *                          overflow on any of them). The presented frame is complete after it.
- * Errors leave the group usable, except a transport failure inside a posted exchange: the group then aborts its
- * communicators and every later call but wcpt_group_destroy returns WCPT_ERROR_DEVICE_LOST.
+ * Errors leave the group usable, except a transport failure inside a posted exchange, and, in a group created with
+ * wcpt_group_create_rank, any wcpt_group_render error while presenting (the other processes still post their part of
+ * the frame's exchange): the group then aborts its communicators and every later call but wcpt_group_destroy returns
+ * WCPT_ERROR_DEVICE_LOST. The other processes' exchange for that frame does not complete; their host ends them.
  * wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains an error. */
 /* The row-block split itself, for a host that runs one process per device (then wcpt_set_row_range with the
  * result): rank r of n renders rows [r*height/n, (r+1)*height/n). Host-only, no device needed. */

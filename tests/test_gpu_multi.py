@@ -383,3 +383,45 @@ def test_group_resize_regrows_payloads_without_device_sync(gpu_ctx):
     for W, H, got in results:
         ref = _context_frames(s, W, H, (0, 1))
         assert np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32)), (W, H)
+
+
+def test_rank_group_of_one_and_unique_id(gpu_ctx):
+    """The one-process-per-device entry points on one GPU: wcpt_group_unique_id gives RCCL's 128-byte id, and a rank
+    group of one (wcpt_group_create_rank with nranks = 1, no communicator needed) renders and presents exactly as a
+    plain context; its info reports one rank, the RCCL transport and no exchange."""
+    uid = wcpt.group_unique_id()
+    assert len(uid) == wcpt._lib.GROUP_UNIQUE_ID_BYTES and any(uid)
+    s = get_scene("cornell")
+    W, H, frames = 40, 30, (0, 1, 2)
+    ref = _context_frames(s, W, H, frames)
+    with wcpt.Group.rank(0, 1, 0, root=0, uid=uid) as g:
+        assert g.context(1) is None
+        ctx = g.context(0)
+        dev = wcpt.DeviceScene(ctx, s)
+        g.create_screen(W, H)
+        nbytes = W * H * 16
+        out = ctx.buffer_alloc(nbytes)
+        g.set_output(wcpt._lib.PAYLOAD_RGBA32F, ctx.buffer_address(out), nbytes)
+        for f in frames:
+            g.render(s.scene_data(W, H, max_bounce=4, frame=f), [dev.materials], [dev.spheres], [dev.draws])
+        g.sync()
+        info = g.info()
+        got = np.frombuffer(ctx.buffer_download(out, nbytes), np.float32).reshape(H, W, 4)
+        ctx.buffer_free(out)
+        dev.free()
+    assert info["nranks"] == 1 and info["local_ranks"] == 1 and info["first_local_rank"] == 0
+    assert info["transport"] == wcpt._lib.GROUP_TRANSPORT_RCCL and info["frames"] == len(frames)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_group_option_and_transport_errors(gpu_ctx):
+    """Unknown group options and transports are refused; the overlap switch can be flipped between frames."""
+    with pytest.raises(wcpt.WcptError):
+        wcpt.Group([0], transport=9)
+    with wcpt.Group([0, 0], transport=COPY) as g:
+        with pytest.raises(wcpt.WcptError):
+            g.set_option(99, 1)
+        g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 0)
+        assert g.info()["overlap"] == 0
+        g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 1)
+        assert g.info()["overlap"] == 1 and g.info()["nranks"] == 2

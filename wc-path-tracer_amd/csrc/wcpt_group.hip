@@ -509,10 +509,13 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
     const size_t nl = g->local.size();
     const bool exchange = presenting(g) && g->nranks > 1;
     const int b = g->overlap ? (int)(g->frames % kPayloadBuffers) : 0;
-    /* 1. every rank's arguments first: an argument error leaves every accumulation image as it was */
+    /* 1. every rank's arguments first: an argument error leaves every accumulation image as it was. In a group whose
+     * other ranks live in other processes, those processes still post their part of this frame's exchange; this one
+     * cannot, so its communicator is aborted (the exchange fails there instead of waiting for a send that never
+     * comes) and the group is unusable -- the collective contract of wcpt_group_create_rank. */
     for (size_t i = 0; i < nl; i++) {
         const int rc = wcpt::render_validate(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
-        if (rc) return rc;
+        if (rc) return (exchange && (int)nl < g->nranks) ? break_group(g, rc) : rc;
     }
     /* 2. point each sender's render at payload b; its previous reader must be done (device-side wait) */
     if (exchange) {
