@@ -349,9 +349,10 @@ def test_group_rank_with_bad_arguments_renders_nothing(gpu_ctx):
 
 
 def test_group_resize_regrows_payloads_without_device_sync(gpu_ctx):
-    """Resizing a 2-rank overlapped group to a larger frame regrows each sender's payload buffers with the stream-ordered
-    allocator while earlier transfers may still be queued; an output too small for the new frame is refused and
-    presenting stops until a new one is set; the next frames equal the one-device frames of the new size."""
+    """Resizing a 2-rank overlapped group to a larger frame regrows each sender's payload buffers while earlier
+    transfers may still be queued (the replaced buffers are retired and freed at the next group-wide wait, with no
+    device synchronisation); an output too small for the new frame is refused and presenting stops until a new one is
+    set; the next frames equal the one-device frames of the new size."""
     s = get_scene("cornell")
     with wcpt.Group([0, 0], transport=COPY) as g:
         devs = [wcpt.DeviceScene(g.context(r), s) for r in range(2)]
@@ -425,3 +426,34 @@ def test_group_option_and_transport_errors(gpu_ctx):
         assert g.info()["overlap"] == 0
         g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 1)
         assert g.info()["overlap"] == 1 and g.info()["nranks"] == 2
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_overlapped_payload_reuse_waits_for_the_previous_transfer(gpu_ctx, kernel):
+    """Event ordering of the overlapped gather: five frames are presented into five different outputs with no wait in
+    between, so frame k+2 rewrites the payload buffer frame k's transfer reads from. Each output must hold exactly its
+    own progressive frame; a payload rewritten before its transfer finished would put frame k+2's rows into output k."""
+    s = get_scene("cornell")
+    W, H, n, frames = 64, 48, 3, (0, 1, 2, 3, 4)
+    nbytes = W * H * 16
+    with wcpt.Group([0] * n, transport=COPY) as g:
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(n)]
+        for r in range(n):
+            g.context(r).set_kernel(kernel)
+        g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 1)
+        g.create_screen(W, H)
+        root = g.context(0)
+        outs = [root.buffer_alloc(nbytes) for _ in frames]
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        for f, o in zip(frames, outs):
+            g.set_output(wcpt._lib.PAYLOAD_RGBA32F, root.buffer_address(o), nbytes)
+            g.render(s.scene_data(W, H, max_bounce=4, frame=f), *addr)
+        g.sync()
+        got = [np.frombuffer(root.buffer_download(o, nbytes), np.float32).reshape(H, W, 4) for o in outs]
+        for o in outs:
+            root.buffer_free(o)
+        for d in devs:
+            d.free()
+    for k, f in enumerate(frames):
+        ref = _context_frames(s, W, H, frames[:k + 1], kernel=kernel)
+        assert np.array_equal(got[k].view(np.uint32), ref.view(np.uint32)), k
