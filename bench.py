@@ -100,8 +100,12 @@ def _profile_json(path, args):
     return None
 
 
-def roofline(args, tot, render_s, frame_s) -> dict:
+def roofline(args, tot, render_s, frame_s, devices=1, ranks=1) -> dict:
     """The dominant kernel against the ceiling of the resource that binds it, measured per render.
+
+    Multi-rank lines price the whole frame's work against the devices it ran on: with one rank per GPU, the slowest
+    rank's block time against `devices` x each per-GPU ceiling; in a rehearsal (several ranks sharing a GPU, whose
+    block renders overlap on it), the frame time against the shared devices' ceilings.
 
     valu_issue (megakernel; c2): SQ_INSTS_VALU wave-instructions per render from the committed SQ counter pass
       (profiles/sq_<config>.json) over the live render time, against the spec issue rate (1024 SIMDs x 2.4 GHz, one
@@ -114,6 +118,9 @@ def roofline(args, tot, render_s, frame_s) -> dict:
       true HBM load, and under not_a_roofline the SURVEY 8(d) algorithmic bytes, which price every scene fetch at HBM
       cost although these scenes are served from L1/L2/MALL."""
     steps = max(1, args.steps)
+    devices = max(1, int(devices))
+    if ranks > devices:
+        render_s = frame_s  # ranks share a device: their block times overlap there and do not add up to its busy time
     alg_bytes = algorithmic_bytes(tot) / steps
     # SURVEY 8(d)'s bytes price every scene fetch at HBM cost, but these scenes are served from L1/L2/MALL, so their
     # rate exceeds the HBM peak: kept for reference, outside the roofline head (every frac there is physical, <= 1)
@@ -126,22 +133,22 @@ def roofline(args, tot, render_s, frame_s) -> dict:
     r["traffic"] = traffic
     if traffic is not None:
         r["hbm_measured_gbs"] = round(traffic / render_s / 1e9, 2)
-        r["hbm_measured_frac"] = round(traffic / render_s / 1e9 / HBM_PEAK_GBS, 4)
+        r["hbm_measured_frac"] = round(traffic / render_s / 1e9 / (HBM_PEAK_GBS * devices), 4)
     sq = _profile_json(os.path.join(ROOT, "profiles", f"sq_{args.config}.json"), args)
     bound = None if sq is None else sq.get("bound")
     if bound == "valu_issue":
         valu = sq["counters_per_launch"]["SQ_INSTS_VALU"] * sq.get("launches_per_frame", 1.0)
         achieved = valu / render_s / 1e9
-        head = {"bound": "valu_issue", "achieved": round(achieved, 1), "peak": VALU_PEAK_GINSTR,
-                "unit": "G wave64 VALU instructions/s", "frac": round(achieved / VALU_PEAK_GINSTR, 3),
+        head = {"bound": "valu_issue", "achieved": round(achieved, 1), "peak": VALU_PEAK_GINSTR * devices,
+                "unit": "G wave64 VALU instructions/s", "frac": round(achieved / (VALU_PEAK_GINSTR * devices), 3),
                 "source": f"SQ_INSTS_VALU {valu:.4g}/render ({sq.get('source', 'profiles')}) over the live render "
                           f"time; peak {SIMDS} SIMDs x {CLOCK_GHZ} GHz / {CYCLES_PER_VALU} cycles"}
         ceil = _valu_mix_ceiling(args.config, getattr(args, "build_id", None))
         if ceil:
             # what this kernel's VALU mix can reach: each instruction class at the fastest rate measured for an
             # instruction of that class (tools/valu_peak.hip; v_add/v_mul/v_mov issue about twice as fast as v_fma)
-            head["measured_ceiling"] = ceil
-            head["measured_frac"] = round(achieved / ceil, 3)
+            head["measured_ceiling"] = round(ceil * devices, 1)
+            head["measured_frac"] = round(achieved / (ceil * devices), 3)
     elif bound == "memory_latency":
         ceil = _gather_ceiling()
         # the line visits the kernels execute: with samples > 1 every sample after the first shades its primary
@@ -150,8 +157,8 @@ def roofline(args, tot, render_s, frame_s) -> dict:
         reused = tot.get("reused_primary_lines", 0)
         lines = (tot["interior_visits"] + tot["triangle_tests"] - reused) / steps
         achieved = lines / frame_s / 1e9
-        head = {"bound": "memory_latency", "achieved": round(achieved, 2), "peak": ceil,
-                "unit": "G dependent line-visits/s", "frac": round(achieved / ceil, 3),
+        head = {"bound": "memory_latency", "achieved": round(achieved, 2), "peak": round(ceil * devices, 2),
+                "unit": "G dependent line-visits/s", "frac": round(achieved / (ceil * devices), 3),
                 "source": "interior visits + triangle tests executed per frame over the frame time (the reference's "
                           "counts less the primary traversals of samples after the first, which reuse sample 0's "
                           "record); peak: dependent random 64-B line visits at 8 waves/SIMD from an L2-resident "
@@ -162,6 +169,8 @@ def roofline(args, tot, render_s, frame_s) -> dict:
         head = {"bound": "unprofiled", "achieved": None, "peak": None, "unit": None, "frac": None,
                 "source": f"no SQ counter pass of this build committed for {args.config} "
                           f"(profiles/sq_{args.config}.json)"}
+    if devices > 1:
+        head["devices"] = devices  # every peak above is the sum over these GPUs
     if STALE_PROFILES:
         head["stale_profiles_refused"] = sorted(set(STALE_PROFILES))
     if sq is not None:
@@ -826,7 +835,7 @@ def main(argv=None):
             "ref_stack": {"overflow_segments": T["ref_stack_overflow_segments"], "max": T["ref_stack_max"],
                           "note": "segments of the timed frames that would write past the reference's uint "
                                   "nodeStack[32] (pathTracer.comp:151), and the deepest stack they reach"},
-            "roofline": roofline(args, T, avg_kernel_s, ms_per_step / 1e3),
+            "roofline": roofline(args, T, avg_kernel_s, ms_per_step / 1e3, devices=distinct, ranks=nranks),
         }
         if nranks > 1:
             out["per_rank_block_ms"] = [b["block_ms"] for b in blocks]

@@ -108,3 +108,22 @@ def test_every_frac_in_the_roofline_head_is_physical(config, kernel, render_ms):
     assert fracs and all(0 < v <= 1.0 for v in fracs.values()), fracs
     assert not any(k.startswith("algorithmic") for k in r)
     assert r["not_a_roofline"]["algorithmic_gbs"] > 0
+
+
+@pytest.mark.parametrize("config,kernel,frame_ms,block_ms", [("c2", 0, 0.07, 0.052), ("c3", 2, 0.75, 0.70)])
+def test_multi_gpu_roofline_prices_the_frame_against_every_device(config, kernel, frame_ms, block_ms):
+    """An 8-GPU line renders one frame over 8 devices: its whole-frame work over the slowest block's time is priced
+    against 8 x each per-GPU ceiling, so every frac stays <= 1 and equals the one-GPU frac of the same per-GPU rate.
+    A rehearsal (4 ranks on one GPU) is priced against that one GPU over the frame time."""
+    tot = _counters(interior_visits=453249769, triangle_tests=104965350, node_pops=915070762, sphere_tests=10 ** 9,
+                    hits=10 ** 7, draw_fetches=10 ** 7, pixels=1920 * 1080)
+    r8 = bench.roofline(_args(config, kernel), dict(tot), block_ms * 1e-3, frame_ms * 1e-3, devices=8, ranks=8)
+    r1 = bench.roofline(_args(config, kernel), dict(tot), 8 * block_ms * 1e-3, 8 * frame_ms * 1e-3)
+    assert r8["devices"] == 8 and "devices" not in r1
+    assert r8["peak"] == pytest.approx(8 * r1["peak"], rel=1e-3)
+    assert r8["frac"] == pytest.approx(r1["frac"], rel=2e-3)
+    fracs = {k: v for k, v in r8.items() if k.endswith("frac") and v is not None}
+    assert fracs and all(0 < v <= 1.0 for v in fracs.values()), fracs
+    reh = bench.roofline(_args(config, kernel), dict(tot), 0.2e-3, 8 * frame_ms * 1e-3, devices=1, ranks=4)
+    whole = bench.roofline(_args(config, kernel), dict(tot), 8 * frame_ms * 1e-3, 8 * frame_ms * 1e-3)
+    assert reh["frac"] == pytest.approx(whole["frac"], rel=2e-3) and "devices" not in reh
