@@ -313,6 +313,9 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          (hipMemcpyPeerAsync of each block into the root's frame, on the sending device's copy
  *                          path; a device may then be listed more than once, so an N-rank group can be rehearsed on
  *                          fewer devices: every rank still has its own context, streams and payloads).
+ *                          Status: the RCCL exchange of a group with n > 1 is UNVERIFIED on hardware here (it needs n
+ *                          distinct GPUs, and the development boxes have one); the COPY transport runs the same
+ *                          bookkeeping (payloads, events, overlap, error paths) and is tested with 2-4 ranks on one GPU.
  *   wcpt_group_unique_id / wcpt_group_create_rank   one process per device (e.g. one process per GPU under
  *                          torchrun): the root's process makes the id (ncclGetUniqueId), the host hands its 128 bytes
  *                          to every process, and each process creates its rank (ncclCommInitRank). RCCL only. All
