@@ -343,6 +343,10 @@ def parse_args(argv=None):
     ap.add_argument("--devices", default=None,
                     help="one-process group: device of each rank, comma-separated (default 0..N-1); a device listed "
                          "more than once rehearses N ranks on fewer GPUs (needs --transport copy)")
+    ap.add_argument("--watchdog-s", type=float, default=900.0,
+                    help="end the process (exit 3, message on stderr) if the run has not finished after this many "
+                         "seconds: a rank whose peer died, or a collective set-up that never completes, must not hang "
+                         "the launcher (0 = off)")
     ap.add_argument("--verify", action="store_true",
                     help="the root re-renders the timed frame sequence on one device and checks the presented frame "
                          "against it bit for bit (adds 'verified' to the JSON line)")
@@ -690,10 +694,31 @@ def verify_frame(args, topo, scene, W, H, spp, bounces, frames: FrameSource, nfr
     return ok
 
 
+def _start_watchdog(seconds, topo):
+    """A daemon timer that ends this process if the run outlives `seconds` (a hung collective: a peer that died, an
+    RCCL set-up that never completes). os._exit, not an exception: the main thread may be blocked inside a device
+    wait. Started before anything touches the GPU; cancelled when the line has been printed."""
+    if not seconds or seconds <= 0:
+        return None
+    import threading
+
+    def fire():
+        sys.stderr.write(f"bench.py: watchdog: rank {topo['rank']} of {topo['nranks']} still running after "
+                         f"{seconds:.0f} s; exiting\n")
+        sys.stderr.flush()
+        os._exit(3)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def main(argv=None):
     global wcpt
     args = parse_args(argv)
     topo = resolve_topology(args, os.environ)
+    watchdog = _start_watchdog(args.watchdog_s, topo)
     if topo["mode"] == "torch":
         import torch  # noqa: F401  (first: libwcpt.so then binds the HIP runtime torch loaded; one runtime per process)
         import torch.distributed as tdist
@@ -860,6 +885,8 @@ def main(argv=None):
     drv.close()
     if rdzv is not None:
         rdzv.close()
+    if watchdog is not None:
+        watchdog.cancel()
 
 
 def hip_runtime_label(mode: str) -> str:

@@ -154,3 +154,18 @@ def test_rendezvous_skips_a_busy_port_and_a_foreign_listener():
         assert got[0] == got[1] == bytes(range(128))
     finally:
         squat.close()
+
+
+def test_watchdog_ends_a_hung_run():
+    """--watchdog-s: a rank stuck past the limit (a peer died in a collective) exits with code 3 and says so, instead of
+    hanging the launcher; a run that finishes in time cancels it."""
+    import subprocess
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "bench._start_watchdog(0.5, {'rank': 1, 'nranks': 2}); time.sleep(30)") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=25)
+    assert p.returncode == 3 and "watchdog: rank 1 of 2" in p.stderr
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "t = bench._start_watchdog(0.5, {'rank': 0, 'nranks': 1}); t.cancel(); time.sleep(1.0)") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=25)
+    assert p.returncode == 0
+    assert bench._start_watchdog(0, {"rank": 0, "nranks": 1}) is None
