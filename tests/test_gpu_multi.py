@@ -457,3 +457,40 @@ def test_overlapped_payload_reuse_waits_for_the_previous_transfer(gpu_ctx, kerne
     for k, f in enumerate(frames):
         ref = _context_frames(s, W, H, frames[:k + 1], kernel=kernel)
         assert np.array_equal(got[k].view(np.uint32), ref.view(np.uint32)), k
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_group_with_a_middle_root_and_presenting_toggled(gpu_ctx, kernel):
+    """Rank 1 of 3 as the root (its own block in the middle of the frame, the blocks of ranks 0 and 2 landing above and
+    below it), 37 rows (blocks of 12, 12 and 13), and presenting switched off for two frames and on again (bench.py's
+    untimed re-render): the ranks keep accumulating while nothing is gathered, and the next presented frame equals the
+    one-device frame of the whole sequence."""
+    s = get_scene("cornell")
+    W, H, n, frames = 44, 37, 3, (0, 1, 2, 3, 4)
+    fmt, px = wcpt._lib.PAYLOAD_RGB32F, 12
+    nbytes = W * H * px
+    with wcpt.Group([0] * n, root=1, transport=COPY) as g:
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(n)]
+        for r in range(n):
+            g.context(r).set_kernel(kernel)
+        g.create_screen(W, H)
+        root = g.context(1)
+        out = root.buffer_from(np.full(nbytes // 4, -3.0, np.float32))
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        g.set_output(fmt, root.buffer_address(out), nbytes)
+        g.render(s.scene_data(W, H, max_bounce=4, frame=0), *addr)
+        g.set_output(0, 0, 0)                      # presenting off: frames 1 and 2 accumulate only
+        for f in (1, 2):
+            g.render(s.scene_data(W, H, max_bounce=4, frame=f), *addr)
+        g.set_output(fmt, root.buffer_address(out), nbytes)
+        for f in (3, 4):
+            g.render(s.scene_data(W, H, max_bounce=4, frame=f), *addr)
+        g.sync()
+        info = g.info()
+        got = np.frombuffer(root.buffer_download(out, nbytes), np.float32).reshape(H, W, 3)
+        root.buffer_free(out)
+        for d in devs:
+            d.free()
+    assert info["root"] == 1 and info["frames"] == len(frames)
+    ref = _context_frames(s, W, H, frames, kernel=kernel)
+    assert np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32))
