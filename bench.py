@@ -704,7 +704,10 @@ def _start_watchdog(seconds, topo):
 
     def fire():
         sys.stderr.write(f"bench.py: watchdog: rank {topo['rank']} of {topo['nranks']} still running after "
-                         f"{seconds:.0f} s; exiting\n")
+                         f"{seconds:.0f} s; exiting. Where every thread was:\n")
+        sys.stderr.flush()
+        import faulthandler
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
         sys.stderr.flush()
         os._exit(3)
 

@@ -75,12 +75,28 @@ def main():
         m, n = counters(a.dir, cfg, filt)
         tot = m.get("SQ_INSTS_VALU")
         frac = {c: m[f"SQ_INSTS_VALU_{c}"] / tot for c in MIX if f"SQ_INSTS_VALU_{c}" in m}
+        packed_note = ""
+        if "SQ_INSTS_VALU_FLOPS_FP32" in m and {"ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32"} <= set(frac):
+            # packed add/mul: FLOPS_FP32 counts FLOPs per lane of each wave-instruction and a packed instruction once
+            # in its class (profiles/valu_flops_calibration.json), so the surplus over ADD + MUL + 2 FMA + TRANS is the
+            # packed adds and multiplies (a packed FMA would add 2: counted as one packed add/mul pair, an upper bound)
+            am = frac["ADD_F32"] + frac["MUL_F32"]
+            surplus = m["SQ_INSTS_VALU_FLOPS_FP32"] / tot - (am + 2 * frac["FMA_F32"] + frac["TRANS_F32"])
+            pk = min(max(surplus, 0.0), am)
+            if am > 0:
+                for c in ("ADD", "MUL"):
+                    share = pk * frac[f"{c}_F32"] / am
+                    frac[f"PK_{c}_F32"] = share
+                    frac[f"{c}_F32"] -= share
+            packed_note = (f"; PK_ADD_F32 / PK_MUL_F32 = the packed forms, from SQ_INSTS_VALU_FLOPS_FP32 "
+                           f"({m['SQ_INSTS_VALU_FLOPS_FP32'] / tot:.3f} FLOPs per lane per VALU instruction: surplus "
+                           f"{surplus:.3f} over one per add/mul/transcendental and two per FMA)")
         frac["other"] = 1.0 - sum(frac.values())
         json.dump({"config": cfg, "kernel": kid, "kernel_name_filter": filt, "dispatches": n.get("SQ_INSTS_VALU_ADD_F32"),
                    "SQ_INSTS_VALU_per_launch": tot, "class_fraction": {k: round(v, 4) for k, v in frac.items()},
                    "build_id": build,
                    "source": src + "; one --pmc pass of SQ_INSTS_VALU and its classes; other = the remainder (moves, "
-                                   "selects, compares, min/max, bit ops)"},
+                                   "selects, compares, min/max, bit ops)" + packed_note},
                   open(os.path.join(a.out, f"valu_mix_{cfg}.json"), "w"), indent=1)
         print(f"{cfg}: build {build}, {filt} {ms:.4f} ms, summaries written")
 
