@@ -39,13 +39,15 @@
 #include <vector>
 
 #include "../../include/wcpt.h"
+#include "group_plan.h"
 #include "pt_kernels.h"
 
 static_assert(sizeof(ncclUniqueId) == WCPT_GROUP_UNIQUE_ID_BYTES, "WCPT_GROUP_UNIQUE_ID_BYTES");
 
 namespace {
 
-constexpr int kPayloadBuffers = 2;
+constexpr int kPayloadBuffers = wcpt::plan::kPayloadBuffers;
+namespace plan = wcpt::plan;
 
 /* One rank driven by this process. */
 struct LocalRank {
@@ -76,6 +78,8 @@ struct wcpt_group {
     int format = 0;                     /* WCPT_PAYLOAD_* of the presented frame; 0 = not presenting */
     uint64_t dst = 0, dst_bytes = 0;    /* the presented frame on the root device (root's process only) */
     uint64_t frames = 0;
+    std::vector<wcpt::plan::RankState> plan_state; /* scratch of wcpt_group_render (no per-frame allocation) */
+    std::vector<wcpt::plan::Step> steps;
 };
 
 namespace {
@@ -508,7 +512,6 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
     if (!g->width) return group_error(WCPT_ERROR_NO_SCREEN, "wcpt_group_render: no screen (wcpt_group_create_screen)");
     const size_t nl = g->local.size();
     const bool exchange = presenting(g) && g->nranks > 1;
-    const int b = g->overlap ? (int)(g->frames % kPayloadBuffers) : 0;
     /* 1. every rank's arguments first: an argument error leaves every accumulation image as it was. In a group whose
      * other ranks live in other processes, those processes still post their part of this frame's exchange; this one
      * cannot, so its communicator is aborted (the exchange fails there instead of waiting for a send that never
@@ -517,90 +520,120 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
         const int rc = wcpt::render_validate(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
         if (rc) return (exchange && (int)nl < g->nranks) ? break_group(g, rc) : rc;
     }
-    /* 2. point each sender's render at payload b; its previous reader must be done (device-side wait) */
-    if (exchange) {
-        for (LocalRank& lr : g->local) {
-            if (lr.rank == g->root) continue;
-            uint32_t y0 = 0, rows = 0;
-            block_of(g, lr.rank, y0, rows);
-            const uint64_t bytes = (uint64_t)g->width * rows * pixel_bytes(g->format);
-            if (!lr.payload[b] || lr.payload_cap[b] < bytes)
+    /* 2-5. the frame's device operations in the order of group_plan.h (tests/test_group_plan.py checks that order on
+     * a simulated device): payload reuse behind the previous transfer, renders, ready events, transfers, sent events */
+    g->plan_state.resize(nl);
+    for (size_t i = 0; i < nl; i++) {
+        g->plan_state[i].rank = g->local[i].rank;
+        for (int k = 0; k < kPayloadBuffers; k++) g->plan_state[i].sent_pending[k] = g->local[i].sent_pending[k];
+    }
+    plan::frame_steps(g->nranks, g->root, g->overlap, exchange, g->transport == WCPT_GROUP_TRANSPORT_COPY, g->frames,
+                      g->plan_state, g->steps);
+    const uint64_t px = exchange ? pixel_bytes(g->format) : 0;
+    auto local_index = [&](int rank) -> size_t {
+        for (size_t i = 0; i < nl; i++)
+            if (g->local[i].rank == rank) return i;
+        return 0; /* the plan names local ranks only */
+    };
+    auto stream_of = [&](LocalRank& lr, int s) {
+        return s == plan::kCommStream ? lr.comm_stream : wcpt::context_stream(lr.ctx);
+    };
+    auto block_bytes = [&](int rank) {
+        uint32_t y0 = 0, rows = 0;
+        block_of(g, rank, y0, rows);
+        return (uint64_t)g->width * rows * px;
+    };
+    auto frame_rows = [&](int rank) {
+        uint32_t y0 = 0, rows = 0;
+        block_of(g, rank, y0, rows);
+        return reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
+    };
+    bool in_group = false; /* inside ncclGroupStart: every transfer argument was fixed above, so a failure below is
+                            * the transport's, and a half-posted exchange is aborted rather than launched */
+    ncclResult_t xfer_err = ncclSuccess;
+    const char* xfer_what = "";
+    size_t renders = 0;
+    for (const plan::Step& st : g->steps) {
+        const size_t i = local_index(st.rank);
+        LocalRank& lr = g->local[i];
+        if (in_group && st.op != plan::kSend && st.op != plan::kRecv) {
+            in_group = false;
+            const ncclResult_t e = ncclGroupEnd();
+            if (xfer_err != ncclSuccess) return break_group(g, nccl_fail(xfer_err, xfer_what));
+            if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupEnd"));
+        }
+        switch (st.op) {
+        case plan::kWaitSent:
+            GHIP(hipSetDevice(lr.device), "hipSetDevice");
+            GHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.sent[st.buffer], 0), "hipStreamWaitEvent(sent)");
+            break;
+        case plan::kSetOutput: {
+            const uint64_t bytes = block_bytes(lr.rank);
+            if (!lr.payload[st.buffer] || lr.payload_cap[st.buffer] < bytes)
                 return group_error(WCPT_ERROR_INVALID_ARGUMENT, "rank %d: payload missing (set the output again)", lr.rank);
-            if (lr.sent_pending[b]) {
-                GHIP(hipSetDevice(lr.device), "hipSetDevice");
-                GHIP(hipStreamWaitEvent(wcpt::context_stream(lr.ctx), lr.sent[b], 0), "hipStreamWaitEvent(sent)");
-            }
-            const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[b]), bytes,
+            const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[st.buffer]), bytes,
                                                   (uint32_t)g->format);
             if (rc) return rc;
+            break;
         }
-    }
-    /* 3. render every rank (validated: a failure now is a device/launch failure, and the ranks are out of step) */
-    for (size_t i = 0; i < nl; i++) {
-        const int rc = wcpt_render(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
-        if (rc) {
-            g->broken = true;
-            return rc;
+        case plan::kRender: {
+            /* validated: a failure now is a device/launch failure, and the ranks are out of step */
+            const int rc = wcpt_render(lr.ctx, scene, materials[i], spheres[i], draw_commands[i]);
+            if (rc) {
+                g->broken = true;
+                return rc;
+            }
+            if (++renders == nl) g->frames++;
+            break;
         }
-    }
-    g->frames++;
-    if (!exchange) return WCPT_SUCCESS; /* the root rendered its block into the output already */
-    /* 4. the gather: senders on their communication streams after their render (or in line), the root receiving */
-    const uint64_t px = pixel_bytes(g->format);
-    for (LocalRank& lr : g->local) {
-        GHIP(hipSetDevice(lr.device), "hipSetDevice");
-        const hipStream_t rs = wcpt::context_stream(lr.ctx);
-        GHIP(hipEventRecord(lr.ready[b], rs), "hipEventRecord(ready)");
-        if (g->overlap && lr.rank != g->root) GHIP(hipStreamWaitEvent(lr.comm_stream, lr.ready[b], 0), "hipStreamWaitEvent");
-    }
-    auto xfer_stream = [&](LocalRank& lr) { return g->overlap ? lr.comm_stream : wcpt::context_stream(lr.ctx); };
-    if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
-        LocalRank& rt = g->local[g->root_local]; /* the COPY transport is single-process: the root is local */
-        for (LocalRank& lr : g->local) {
-            if (lr.rank == g->root) continue;
-            uint32_t y0 = 0, rows = 0;
-            block_of(g, lr.rank, y0, rows);
-            void* at = reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
+        case plan::kRecordReady:
             GHIP(hipSetDevice(lr.device), "hipSetDevice");
-            GHIP(hipMemcpyPeerAsync(at, rt.device, lr.payload[b], lr.device, (uint64_t)g->width * rows * px,
-                                    xfer_stream(lr)),
-                 "hipMemcpyPeerAsync(block)");
-        }
-    } else {
-        /* every argument was checked above, so no call below can fail on its arguments; a failure here is the
-         * transport's, and a half-posted exchange is aborted rather than launched */
-        ncclResult_t e = ncclGroupStart();
-        if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupStart"));
-        ncclResult_t first = ncclSuccess;
-        const char* what = "";
-        for (LocalRank& lr : g->local) {
-            if (first != ncclSuccess) break;
-            if (lr.rank != g->root) {
-                uint32_t y0 = 0, rows = 0;
-                block_of(g, lr.rank, y0, rows);
-                first = ncclSend(lr.payload[b], (uint64_t)g->width * rows * px, ncclUint8, g->root, lr.comm, xfer_stream(lr));
-                what = "ncclSend";
-                continue;
+            GHIP(hipEventRecord(lr.ready[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(ready)");
+            break;
+        case plan::kCommWaitReady:
+            GHIP(hipSetDevice(lr.device), "hipSetDevice");
+            GHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.ready[st.buffer], 0), "hipStreamWaitEvent(ready)");
+            break;
+        case plan::kSend:
+            if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
+                const LocalRank& rt = g->local[g->root_local]; /* the COPY transport is single-process */
+                GHIP(hipSetDevice(lr.device), "hipSetDevice");
+                GHIP(hipMemcpyPeerAsync(frame_rows(lr.rank), rt.device, lr.payload[st.buffer], lr.device,
+                                        block_bytes(lr.rank), stream_of(lr, st.stream)),
+                     "hipMemcpyPeerAsync(block)");
+                break;
             }
-            for (int r = 0; r < g->nranks && first == ncclSuccess; r++) {
-                if (r == g->root) continue;
-                uint32_t y0 = 0, rows = 0;
-                block_of(g, r, y0, rows);
-                void* at = reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
-                first = ncclRecv(at, (uint64_t)g->width * rows * px, ncclUint8, r, lr.comm,
-                                 g->overlap ? lr.comm_stream : wcpt::context_stream(lr.ctx));
-                what = "ncclRecv";
+            /* fall through */
+        case plan::kRecv:
+            if (!in_group) {
+                const ncclResult_t e = ncclGroupStart();
+                if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupStart"));
+                in_group = true;
             }
+            if (xfer_err != ncclSuccess) break; /* skip the rest; the group is ended and aborted below */
+            if (st.op == plan::kSend) {
+                xfer_err = ncclSend(lr.payload[st.buffer], block_bytes(lr.rank), ncclUint8, st.peer, lr.comm,
+                                    stream_of(lr, st.stream));
+                xfer_what = "ncclSend";
+            } else {
+                xfer_err = ncclRecv(frame_rows(st.peer), block_bytes(st.peer), ncclUint8, st.peer, lr.comm,
+                                    stream_of(lr, st.stream));
+                xfer_what = "ncclRecv";
+            }
+            break;
+        case plan::kRecordSent:
+            GHIP(hipSetDevice(lr.device), "hipSetDevice");
+            GHIP(hipEventRecord(lr.sent[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(sent)");
+            lr.sent_pending[st.buffer] = true;
+            break;
+        default:
+            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group plan step %d", st.op);
         }
-        e = ncclGroupEnd();
-        if (first != ncclSuccess) return break_group(g, nccl_fail(first, what));
-        if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupEnd"));
     }
-    for (LocalRank& lr : g->local) {
-        if (lr.rank == g->root) continue;
-        GHIP(hipSetDevice(lr.device), "hipSetDevice");
-        GHIP(hipEventRecord(lr.sent[b], xfer_stream(lr)), "hipEventRecord(sent)");
-        lr.sent_pending[b] = true;
+    if (in_group) { /* a process holding only the root: its receives end the plan */
+        const ncclResult_t e = ncclGroupEnd();
+        if (xfer_err != ncclSuccess) return break_group(g, nccl_fail(xfer_err, xfer_what));
+        if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupEnd"));
     }
     return WCPT_SUCCESS;
 }
