@@ -10,8 +10,10 @@ python3 -c "import sys; sys.path.insert(0, 'wc-path-tracer_amd'); import wcpt; p
 for cfg in ${CONFIGS:-c2 ref c3 c4}; do
   B="--config $cfg --no-cpu-baseline --steps 2 --warmup 1"
   [ "$cfg" = c4 ] && B="--config $cfg --no-cpu-baseline --steps 1 --warmup 0 --settle-ms 0"
-  PS=20; [ "$cfg" = c3 ] && PS=10; [ "$cfg" = c4 ] && PS=2
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$cfg" -o $cfg -- python3 bench.py --config $cfg --no-cpu-baseline --steps $PS --warmup 2 > "$OUT/prof_$cfg.log" 2>&1 || { echo "prof $cfg failed"; tail -3 "$OUT/prof_$cfg.log"; exit 1; }
+  # the kernel-stats run is the bench line's own command (tools/gpu_r04_session.sh: default steps and warmup, c4 20 + 3),
+  # so the rocprof average covers the same frames under the same sustained load as the bench's HIP events
+  PB=""; [ "$cfg" = c4 ] && PB="--steps 20 --warmup 3"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$cfg" -o $cfg -- python3 bench.py --config $cfg --no-cpu-baseline $PB > "$OUT/prof_$cfg.log" 2>&1 || { echo "prof $cfg failed"; tail -3 "$OUT/prof_$cfg.log"; exit 1; }
   echo "prof $cfg ok"
   n=0
   PASSES=("FETCH_SIZE" "WRITE_SIZE" \
