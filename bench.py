@@ -436,7 +436,14 @@ class GroupBench:
         else:
             uid = wcpt.group_unique_id() if topo["rank"] == 0 else None
             uid = rdzv.broadcast(uid)
-            self.g = wcpt.Group.rank(topo["local_rank"], topo["nranks"], topo["rank"], root=0, uid=uid)
+            # LOCAL_RANK names the device; a launcher that shows each process fewer devices (one per process) gets
+            # its LOCAL_RANK folded onto what it sees
+            dev = topo["local_rank"]
+            seen = wcpt.device_count()
+            if seen > 0 and dev >= seen:
+                dev %= seen
+            topo["devices"] = [dev]
+            self.g = wcpt.Group.rank(dev, topo["nranks"], topo["rank"], root=0, uid=uid)
         self.ctxs = self.g.contexts
         self.ranks = self.g.ranks
         self.devs = []
@@ -694,6 +701,13 @@ def verify_frame(args, topo, scene, W, H, spp, bounces, frames: FrameSource, nfr
     return ok
 
 
+def _gpu_identity(device: int) -> str:
+    try:
+        return wcpt.device_pci_bus_id(device)
+    except Exception:  # an older library or a runtime without the query: the ordinal, this process's view
+        return f"ordinal {device}"
+
+
 def _start_watchdog(seconds, topo):
     """A daemon timer that ends this process if the run outlives `seconds` (a hung collective: a peer that died, an
     RCCL set-up that never completes). os._exit, not an exception: the main thread may be blocked inside a device
@@ -797,6 +811,7 @@ def main(argv=None):
     per_rank = [{"rank": int(r), "block_ms": round(ms / max(1, n), 4), "launches": int(n)}
                 for r, (ms, n) in zip(drv.ranks, prof)]
     mine = {"elapsed": elapsed, "tot": tot, "per_rank": per_rank, "devices": [int(c.device) for c in drv.ctxs],
+            "gpus": [_gpu_identity(int(c.device)) for c in drv.ctxs],
             "kernel_ms": sum(ms for ms, _ in prof), "launches": sum(n for _, n in prof)}
     allr = coll.gather_obj(json.loads(json.dumps(mine, default=int)))
 
@@ -817,7 +832,9 @@ def main(argv=None):
         segs_all, prim_all = float(T["segments"]), float(T["pixels"] * spp)
         value = segs_all / elapsed_max / 1e6
         info = drv.info()
-        distinct = len({dv for a in allr for dv in a["devices"]})  # GPUs the ranks ran on (a rehearsal repeats one)
+        # physical GPUs the ranks ran on, by PCI bus id (device ordinals differ between processes that see different
+        # devices; a rehearsal repeats one GPU)
+        distinct = len({gp for a in allr for gp in a["gpus"]})
         kind = {"group": "one process, one host thread, all ranks (wcpt_group_create_ex)",
                 "ranks": "one process per GPU (wcpt_group_create_rank, ncclCommInitRank; host rendezvous wcpt.rdzv)",
                 "torch": f"one process per GPU, torch.distributed {args.dist_backend} gather (rehearsal path)"}

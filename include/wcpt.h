@@ -231,6 +231,9 @@ int         wcpt_abi_version(void);
  * counter profile) can tell whether they describe the library that is loaded. */
 const char* wcpt_build_id(void);
 int         wcpt_device_count(int* count);
+/* The PCI bus id of a device ("dddd:bb:dd.f", NUL-terminated in out[0..len)): identifies a GPU across processes that
+ * see different device ordinals (e.g. a launcher that makes one device visible per process). */
+int         wcpt_device_pci_bus_id(int device, char* out, int len);
 int         wcpt_create(int device, wcpt_context** out_ctx);
 int         wcpt_destroy(wcpt_context* ctx);                       /* Deinit, PathTracingRenderer.jai:473 */
 const char* wcpt_last_error(const wcpt_context* ctx);              /* ctx may be NULL: last global error */

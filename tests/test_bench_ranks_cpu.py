@@ -17,14 +17,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 UID = bytes((7 * i) % 256 for i in range(128))
 
 
-def _fake_wcpt(rank, nranks, log):
-    """The slice of the wcpt package bench.py uses in its group modes, recording what it was asked to do."""
+def _fake_wcpt(rank, nranks, log, one_visible=False):
+    """The slice of the wcpt package bench.py uses in its group modes, recording what it was asked to do.
+    one_visible: the launcher shows each process only its own GPU (device 0 everywhere, distinct PCI ids)."""
     import wcpt._lib as L
     from wcpt import scene as real_scene
 
     class Ctx:
         def __init__(self, rows):
-            self.rows, self.prof, self.device = rows, [], rank
+            self.rows, self.prof, self.device = rows, [], 0 if one_visible else rank
 
         def set_kernel(self, k):
             log.append(("kernel", k))
@@ -63,7 +64,7 @@ def _fake_wcpt(rank, nranks, log):
 
         @classmethod
         def rank(cls, device, n, r, root=0, uid=None):
-            assert (device, n, r, root) == (rank, nranks, rank, 0)
+            assert (device, n, r, root) == (0 if one_visible else rank, nranks, rank, 0)
             assert uid == UID, "the RCCL id must reach every rank unchanged"
             log.append(("group", device, n, r))
             return cls(Ctx(5 if r == 0 else 4), r)
@@ -112,20 +113,23 @@ def _fake_wcpt(rank, nranks, log):
     m.group_unique_id = lambda: UID
     m.runtime_version = lambda: 70226015
     m.build_id = lambda: "stand-in"
+    # torchrun: every process sees every GPU, so LOCAL_RANK is the device; one_visible: each sees one, its own
+    m.device_count = lambda: 1 if one_visible else nranks
+    m.device_pci_bus_id = lambda d: f"0000:{0x11 + 0x20 * (rank if one_visible else d):02x}:00.0"
     # bench.py calls wcpt_group_render through the library with prebuilt arrays: route it to the stand-in group
     m.lib = types.SimpleNamespace(wcpt_group_render=lambda h, sd, mm, ss, dd: h.render(sd, list(mm), list(ss), list(dd)))
     m.SCENE_DATA_DTYPE = L.SCENE_DATA_DTYPE
     return m
 
 
-def _rank_main(rank, world, port, out_dir):
+def _rank_main(rank, world, port, out_dir, one_visible=False):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "wc-path-tracer_amd")]
     os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port - 1))
     import wcpt  # noqa: F401  (the real package: its scene module builds the Cornell box on the host)
     import wcpt.rdzv  # noqa: F401  (the real rendezvous, which stays registered under its name)
     log = []
-    sys.modules["wcpt"] = _fake_wcpt(rank, world, log)
+    sys.modules["wcpt"] = _fake_wcpt(rank, world, log, one_visible)
     import bench
     out = open(os.path.join(out_dir, f"rank{rank}.out"), "w")
     sys.stdout = out
@@ -143,11 +147,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_bench_one_process_per_gpu_plumbing(tmp_path, world):
+@pytest.mark.parametrize("world,one_visible", [(2, False), (3, False), (3, True)])
+def test_bench_one_process_per_gpu_plumbing(tmp_path, world, one_visible):
+    """one_visible: a launcher that shows each process only its GPU -- LOCAL_RANK folds onto device 0, and n_gpus still
+    counts the distinct GPUs (by PCI bus id), not the ordinals the processes see."""
     ctx = mproc.get_context("spawn")
     port = _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path), one_visible)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -171,7 +177,7 @@ def test_bench_one_process_per_gpu_plumbing(tmp_path, world):
     assert d["value"] > 0 and d["ms_per_step"] > 0
     logs = [json.load(open(tmp_path / f"rank{r}.log")) for r in range(world)]
     for r, log in enumerate(logs):
-        assert ["group", r, world, r] in log and ["closed"] in log
+        assert ["group", 0 if one_visible else r, world, r] in log and ["closed"] in log
         assert ["set_output", 3, r == 0] in log                      # rgb payloads; only the root names a frame
         assert (["output", 256 * 256 * 12] in log) == (r == 0)         # c1: 256x256, rgb 12 B/px, on the root
         assert ["set_output", 0, False] in log                         # presenting off for the untimed re-render

@@ -645,6 +645,18 @@ int wcpt_device_count(int* count)
     return WCPT_SUCCESS;
 }
 
+int wcpt_device_pci_bus_id(int device, char* out, int len)
+{
+    if (!out || len < 13) return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "pci bus id buffer of %d bytes", len);
+    const hipError_t e = hipDeviceGetPCIBusId(out, len, device);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        out[0] = 0;
+        return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "hipDeviceGetPCIBusId(%d): %s", device, hipGetErrorString(e));
+    }
+    return WCPT_SUCCESS;
+}
+
 int wcpt_create(int device, wcpt_context** out_ctx)
 {
     if (!out_ctx) return set_error(nullptr, WCPT_ERROR_INVALID_ARGUMENT, "null out_ctx");

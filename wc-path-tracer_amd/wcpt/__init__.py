@@ -14,7 +14,7 @@ __all__ = [
     "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
-    "PathTracingRenderer", "Editor", "Group", "group_unique_id", "scene", "device_count", "runtime_version", "build_id",
+    "PathTracingRenderer", "Editor", "Group", "group_unique_id", "scene", "device_count", "device_pci_bus_id", "runtime_version", "build_id",
 ]
 
 
@@ -23,6 +23,14 @@ def device_count() -> int:
     n = C.c_int()
     lib.wcpt_device_count(C.byref(n))
     return n.value
+
+
+def device_pci_bus_id(device: int) -> str:
+    """wcpt_device_pci_bus_id: the GPU's PCI bus id, the same in every process whatever its device ordinals."""
+    import ctypes as C
+    buf = C.create_string_buffer(64)
+    _lib.check(lib.wcpt_device_pci_bus_id(device, buf, 64))
+    return buf.value.decode()
 
 
 def build_id() -> str:

@@ -135,6 +135,7 @@ _PROTOTYPES = {
     "wcpt_abi_version": (_i, []),
     "wcpt_build_id": (C.c_char_p, []),
     "wcpt_device_count": (_i, [C.POINTER(_i)]),
+    "wcpt_device_pci_bus_id": (_i, [_i, C.c_char_p, _i]),
     "wcpt_create": (_i, [_i, C.POINTER(_p)]),
     "wcpt_destroy": (_i, [_p]),
     "wcpt_last_error": (C.c_char_p, [_p]),
