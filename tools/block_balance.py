@@ -1,5 +1,6 @@
 """Load balance of the N-way row-block split on ONE GPU: every rank's block of a bench config rendered in turn
-(same kernel, options and progressive frames as bench.py), timed with HIP events on the context stream.
+(same kernel, options and progressive frames as bench.py), timed with HIP events on the context stream, on the
+system HIP runtime that bench.py binds (torch is not imported).
 
     python tools/block_balance.py [--config c2] [--ns 2,4,8] [--frames 20] [--rounds 3]
 
@@ -9,7 +10,6 @@ full-frame / N (perfect split). max / (full / N) is the load-balance + tail loss
 import argparse
 import os
 
-import torch  # noqa: F401  (bench.py's load order: libwcpt binds to torch's HIP runtime)
 import statistics
 import sys
 

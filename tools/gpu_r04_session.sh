@@ -23,4 +23,8 @@ if [ "${GROUP:-1}" = 1 ]; then
   run group_c3_g3copy 300 python3 -u bench.py --config c3 --no-cpu-baseline --gpus 3 --devices 0,0,0 --transport copy --verify --gather display --steps 10 --warmup 3
   run torch_gloo_c2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --dist-backend gloo --verify --steps 20 --warmup 5 --watchdog-s 120
 fi
+if [ "${BALANCE:-1}" = 1 ]; then
+  run balance_c2 300 python3 -u tools/block_balance.py --config c2 --ns 2,4,8
+  run balance_c3 300 python3 -u tools/block_balance.py --config c3 --ns 2,4,8
+fi
 echo SESSION_DONE
