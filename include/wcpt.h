@@ -227,8 +227,9 @@ typedef uint64_t wcpt_buffer;      /* 0 is never a valid handle */
 
 /* ---- library / context ---------------------------------------------------------------------------- */
 int         wcpt_abi_version(void);
-/* Identity of this build's sources and compile flags (a short hash): measurements recorded against one build (e.g. a
- * counter profile) can tell whether they describe the library that is loaded. */
+/* Identity of the sources and compile flags that decide this build's kernels and their launches (a short hash; the
+ * multi-device group's exchange code and this header's comments are left out): measurements recorded against one
+ * build (e.g. a counter profile) can tell whether they describe the kernels of the library that is loaded. */
 const char* wcpt_build_id(void);
 int         wcpt_device_count(int* count);
 /* The PCI bus id of a device ("dddd:bb:dd.f", NUL-terminated in out[0..len)): identifies a GPU across processes that
