@@ -29,11 +29,12 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--first", action="store_true", help="rank 0's block only (a size sweep)")
+    ap.add_argument("--kernel", type=int, default=-1, help="WCPT_KERNEL_* (default: bench.py's for the config)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
     ctx = wcpt.Context(0)
-    ctx.set_kernel(bench.DEFAULT_KERNEL[a.config])
+    ctx.set_kernel(bench.DEFAULT_KERNEL[a.config] if a.kernel < 0 else a.kernel)
     dev = wcpt.DeviceScene(ctx, s)
     ctx.create_screen(W, H)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
@@ -53,7 +54,8 @@ def main():
         return statistics.median(out)
 
     full = timed(0, H)
-    print(f"{a.config}: {desc}; full frame {full:.4f} ms", flush=True)
+    print(f"{a.config}: {desc}; kernel {bench.DEFAULT_KERNEL[a.config] if a.kernel < 0 else a.kernel}; "
+          f"full frame {full:.4f} ms", flush=True)
     for n in [int(x) for x in a.ns.split(",")]:
         t = [timed(*row_block(H, n, r)) for r in range(1 if a.first else n)]
         mx, mean = max(t), sum(t) / len(t)
