@@ -859,7 +859,7 @@ def main(argv=None):
                        "frames": ("progressive, renderedFramesCount=warmup.." if args.camera == "still" else
                                   "moving camera (editor strafe + yaw every frame), renderedFramesCount=0"),
                        "camera": args.camera,
-                       "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel], "bvh": args.bvh,
+                       "kernel": {0: "megakernel", 1: "auto", 2: "wavefront"}[args.kernel], "bvh": args.bvh,
                        "parallelism": (f"row-block x{nranks} + {transport} gather of {args.gather} blocks"
                                        + ("" if args.no_overlap else " overlapped with the next frame")
                                        if nranks > 1 else "one device")},

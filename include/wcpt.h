@@ -60,6 +60,10 @@ extern "C" {
 /* ---- kernel variants ---------------------------------------------------------------------------- */
 #define WCPT_KERNEL_MEGAKERNEL  0  /* one lane per pixel, exact reference semantics (default)          */
 #define WCPT_KERNEL_WAVEFRONT   2  /* split ray-gen / traverse / shade queues (same semantics)         */
+/* Chosen per render from the scene: the megakernel where the draws' leaves hold several triangles each (the pair-record
+ * layout: Cornell-class and the reference's mushroom), the wavefront kernel for thin-leaf meshes (a Sponza-scale
+ * midpoint BVH, ~2 triangles per leaf), the faster of the two on every bench scene. Same results either way. */
+#define WCPT_KERNEL_AUTO        1
 
 /* ---- tuning options (wcpt_set_option); none changes results ------------------------------------- */
 #define WCPT_OPTION_STACK       1  /* megakernel traversal stack: 0 = scratch, 1 = LDS + spill (default) */
@@ -240,6 +244,7 @@ int         wcpt_destroy(wcpt_context* ctx);                       /* Deinit, Pa
 const char* wcpt_last_error(const wcpt_context* ctx);              /* ctx may be NULL: last global error */
 int         wcpt_set_stream(wcpt_context* ctx, void* hip_stream);  /* NULL: the context's own stream     */
 int         wcpt_set_kernel(wcpt_context* ctx, int variant);       /* WCPT_KERNEL_*                       */
+int         wcpt_last_kernel(wcpt_context* ctx, int* variant);     /* what the last render ran (AUTO resolved) */
 int         wcpt_set_option(wcpt_context* ctx, int option, int value); /* WCPT_OPTION_*                   */
 
 /* ---- device buffers (BufferManager.jai) ------------------------------------------------------------ */

@@ -252,3 +252,29 @@ def test_bvh_rewritten_behind_the_triangle_cache_stays_in_bounds(gpu_ctx):
         gpu_ctx.set_option(wcpt._lib.OPTION_TRIANGLE_CACHE, 1)
         gpu_ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
         dev.free()
+
+
+@pytest.mark.parametrize("name,expect", [("cornell", wcpt.KERNEL_MEGAKERNEL), ("reference_init", wcpt.KERNEL_MEGAKERNEL),
+                                         ("atrium", wcpt.KERNEL_WAVEFRONT)])
+def test_kernel_auto_picks_per_scene_and_renders_the_same_frames(gpu_ctx, name, expect):
+    """WCPT_KERNEL_AUTO resolves per render from the draws' leaf layout: the megakernel where leaves hold several
+    triangles (Cornell, the reference's mushroom), the wavefront kernel on the atrium's thin leaves -- the faster kernel
+    on each bench scene -- and the frames equal the explicitly chosen kernel's bit for bit."""
+    s = get_scene(name)
+    W, H = 96, 64
+    imgs = {}
+    for k in (wcpt.KERNEL_AUTO, expect):
+        with wcpt.Context(0) as ctx:
+            dev = wcpt.DeviceScene(ctx, s)
+            ctx.set_kernel(k)
+            ctx.create_screen(W, H)
+            for f in (0, 1):
+                ctx.render(s.scene_data(W, H, max_bounce=3, frame=f), *dev.addresses())
+            ctx.sync()
+            imgs[k] = (ctx.readback(), ctx.last_kernel())
+            dev.free()
+    assert imgs[wcpt.KERNEL_AUTO][1] == expect and imgs[expect][1] == expect
+    assert np.array_equal(imgs[wcpt.KERNEL_AUTO][0].view(np.uint32), imgs[expect][0].view(np.uint32))
+    with wcpt.Context(0) as ctx:
+        with pytest.raises(wcpt.WcptError):
+            ctx.set_kernel(3)

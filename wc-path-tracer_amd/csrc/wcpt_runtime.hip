@@ -145,6 +145,7 @@ struct wcpt_context {
     uint32_t* d_scan = nullptr;        /* leaf-count scan flag (prepare_tri_records) */
     uint64_t scratch_bytes = 0;
     int kernel = WCPT_KERNEL_MEGAKERNEL;
+    int kernel_run = WCPT_KERNEL_MEGAKERNEL; /* the variant the current/last render runs (WCPT_KERNEL_AUTO resolved) */
     int stack_kind = 1;                /* WCPT_OPTION_STACK: 0 scratch, 1 LDS + spill (default; c2 -2%, 135-row blocks -8%) */
     int diagnostics = 0;               /* WCPT_OPTION_DIAGNOSTICS */
     int sort_rays = 0;                 /* WCPT_OPTION_SORT_RAYS (wavefront only; measured a net loss on c3) */
@@ -381,8 +382,13 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
     a.pair_records = tris_max <= kPairMaxTriangles &&
                      (ctx->pair_records == 1 ||
                       (ctx->pair_records < 0 && leaves_all > 0 && (double)tris_all >= kPairMinTrianglesPerLeaf * leaves_all));
+    /* WCPT_KERNEL_AUTO: the megakernel where leaves hold several triangles (its pair loops and scalar-cache leaves pay),
+     * the wavefront kernel on thin leaves (Cornell 0.37 / mushroom 1.22 ms megakernel against 2.0 ms wavefront on the
+     * mushroom; the atrium 4.8 ms wavefront against 9.8 ms megakernel) */
+    ctx->kernel_run = ctx->kernel != WCPT_KERNEL_AUTO ? ctx->kernel
+                                                      : (a.pair_records || n == 0 ? WCPT_KERNEL_MEGAKERNEL : WCPT_KERNEL_WAVEFRONT);
     /* primary-ray pair records (megakernel with pair records): derived once per camera position and records build */
-    const bool want_primary = kPrimaryPairs && a.pair_records && ctx->kernel == WCPT_KERNEL_MEGAKERNEL;
+    const bool want_primary = kPrimaryPairs && a.pair_records && ctx->kernel_run == WCPT_KERNEL_MEGAKERNEL;
     uint32_t origin[3];
     std::memcpy(origin, sd.position, sizeof(origin));
     for (uint32_t d = 0; d < n; d++) {
@@ -510,15 +516,15 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     if (rc) return rc;
 #if WCPT_MK_TIMERS
     /* tools-only build: the render's megakernel adds its phase timers to the counters (wcpt_read_diagnostics) */
-    if (mode == wcpt::kModeRender && ctx->kernel == WCPT_KERNEL_MEGAKERNEL)
+    if (mode == wcpt::kModeRender && ctx->kernel_run == WCPT_KERNEL_MEGAKERNEL)
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream),
                 "hipMemsetAsync(timers)");
 #endif
     hipError_t e = hipSuccess;
-    switch (ctx->kernel) {
+    switch (ctx->kernel_run) {
     case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->mk, ctx->stream); break;
     case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->wf_pipes, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream); break;
-    default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel);
+    default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel_run);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
     if (e1) HIP_TRY(ctx, hipEventRecord(e1, ctx->stream), "hipEventRecord");
@@ -726,9 +732,17 @@ int wcpt_set_stream(wcpt_context* ctx, void* hip_stream)
 int wcpt_set_kernel(wcpt_context* ctx, int variant)
 {
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
-    if (variant != WCPT_KERNEL_MEGAKERNEL && variant != WCPT_KERNEL_WAVEFRONT)
+    if (variant != WCPT_KERNEL_MEGAKERNEL && variant != WCPT_KERNEL_WAVEFRONT && variant != WCPT_KERNEL_AUTO)
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", variant);
     ctx->kernel = variant;
+    return WCPT_SUCCESS;
+}
+
+int wcpt_last_kernel(wcpt_context* ctx, int* variant)
+{
+    if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    if (!variant) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null variant");
+    *variant = ctx->kernel_run;
     return WCPT_SUCCESS;
 }
 
@@ -1086,7 +1100,7 @@ int wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n)
     if (!out || n > 8) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_read_diagnostics: bad output");
     memset(out, 0, sizeof(uint64_t) * n);
 #if WCPT_MK_TIMERS
-    if (ctx->kernel == WCPT_KERNEL_MEGAKERNEL && n) { /* megakernel phase timers of the last render */
+    if (ctx->kernel_run == WCPT_KERNEL_MEGAKERNEL && n) { /* megakernel phase timers of the last render */
         HIP_TRY(ctx, hipMemcpyAsync(out, ctx->d_counters, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream),
                 "hipMemcpyAsync(timers)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");

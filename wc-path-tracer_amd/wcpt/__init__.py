@@ -3,7 +3,7 @@
 The compute lives in libwcpt.so (hand-written HIP for gfx950 behind the C-ABI of include/wcpt.h); this
 package is the Python host mirror used by tests and the benchmark.
 """
-from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_MEGAKERNEL,
+from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, EXPORTED_SYMBOLS, KERNEL_AUTO, KERNEL_MEGAKERNEL,
                    KERNEL_WAVEFRONT, LIB_PATH, MATERIAL_DIELECTRIC, MATERIAL_DTYPE, MATERIAL_METAL, NODE_DTYPE,
                    SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, WcptError, lib)
 from .renderer import Context, DeviceScene, Editor, Group, PathTracingRenderer, group_unique_id
@@ -11,7 +11,7 @@ from . import scene
 from . import _lib
 
 __all__ = [
-    "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_MEGAKERNEL",
+    "COUNTER_FIELDS", "DRAW_COMMAND_DTYPE", "EXPORTED_SYMBOLS", "KERNEL_AUTO", "KERNEL_MEGAKERNEL",
     "KERNEL_WAVEFRONT", "LIB_PATH", "MATERIAL_DIELECTRIC", "MATERIAL_DTYPE", "MATERIAL_METAL", "NODE_DTYPE",
     "SCENE_DATA_DTYPE", "SPHERE_DTYPE", "Camera", "WcptError", "lib", "Context", "DeviceScene",
     "PathTracingRenderer", "Editor", "Group", "group_unique_id", "scene", "device_count", "device_pci_bus_id", "runtime_version", "build_id",

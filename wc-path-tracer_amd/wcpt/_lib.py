@@ -39,6 +39,7 @@ MATERIAL_DIELECTRIC = 1
 
 KERNEL_MEGAKERNEL = 0
 KERNEL_WAVEFRONT = 2
+KERNEL_AUTO = 1
 
 OPTION_STACK = 1
 OPTION_DIAGNOSTICS = 2
@@ -135,6 +136,7 @@ _PROTOTYPES = {
     "wcpt_abi_version": (_i, []),
     "wcpt_build_id": (C.c_char_p, []),
     "wcpt_device_count": (_i, [C.POINTER(_i)]),
+    "wcpt_last_kernel": (_i, [_p, C.POINTER(_i)]),
     "wcpt_device_pci_bus_id": (_i, [_i, C.c_char_p, _i]),
     "wcpt_create": (_i, [_i, C.POINTER(_p)]),
     "wcpt_destroy": (_i, [_p]),

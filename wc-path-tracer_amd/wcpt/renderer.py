@@ -58,6 +58,12 @@ class Context:
     def set_kernel(self, variant: int):
         self._chk(lib.wcpt_set_kernel(self.h, variant))
 
+    def last_kernel(self) -> int:
+        """The variant the last render ran (WCPT_KERNEL_AUTO resolved per render)."""
+        v = C.c_int()
+        self._chk(lib.wcpt_last_kernel(self.h, C.byref(v)))
+        return v.value
+
     def set_option(self, option: int, value: int):
         self._chk(lib.wcpt_set_option(self.h, option, value))
 
