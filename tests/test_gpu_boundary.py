@@ -278,3 +278,36 @@ def test_kernel_auto_picks_per_scene_and_renders_the_same_frames(gpu_ctx, name, 
     with wcpt.Context(0) as ctx:
         with pytest.raises(wcpt.WcptError):
             ctx.set_kernel(3)
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_checkpoint_and_resume_progressive_accumulation(gpu_ctx, kernel):
+    """Checkpoint / resume: the accumulation state is the float4 image plus renderedFramesCount. Read it
+    back after frame 2, destroy the context, seed a new one with wcpt_image_upload and continue with frames 3 and 4:
+    the image equals an uninterrupted sequence's, bit for bit."""
+    s = get_scene("cornell")
+    W, H = 80, 48
+    sds = [s.scene_data(W, H, max_bounce=4, frame=f) for f in range(5)]
+    with wcpt.Context(0) as a:
+        dev = wcpt.DeviceScene(a, s)
+        a.set_kernel(kernel)
+        a.create_screen(W, H)
+        for f in range(5):
+            a.render(sds[f], *dev.addresses())
+            if f == 2:
+                a.sync()
+                checkpoint = a.readback().copy()
+        a.sync()
+        whole = a.readback()
+        dev.free()
+    with wcpt.Context(0) as b:
+        dev = wcpt.DeviceScene(b, s)
+        b.set_kernel(kernel)
+        b.create_screen(W, H)
+        b.image_upload(checkpoint)
+        for f in (3, 4):
+            b.render(sds[f], *dev.addresses())
+        b.sync()
+        resumed = b.readback()
+        dev.free()
+    assert np.array_equal(resumed.view(np.uint32), whole.view(np.uint32))
