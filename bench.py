@@ -771,6 +771,9 @@ def main(argv=None):
     for f in range(args.warmup):
         drv.render(frames(f))
     drv.sync()
+    args.kernel_auto = args.kernel == wcpt.KERNEL_AUTO
+    if args.kernel_auto:  # the variant the library chose for this scene: the profiles and the line name that one
+        args.kernel = int(drv.ctxs[0].last_kernel())
     coll.barrier()
     drv.sync()
     # Kernel time for the roofline: HIP events around every render on each rank's render stream. With one rank they
@@ -859,7 +862,8 @@ def main(argv=None):
                        "frames": ("progressive, renderedFramesCount=warmup.." if args.camera == "still" else
                                   "moving camera (editor strafe + yaw every frame), renderedFramesCount=0"),
                        "camera": args.camera,
-                       "kernel": {0: "megakernel", 1: "auto", 2: "wavefront"}[args.kernel], "bvh": args.bvh,
+                       "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel] +
+                                 (" (WCPT_KERNEL_AUTO's choice)" if args.kernel_auto else ""), "bvh": args.bvh,
                        "parallelism": (f"row-block x{nranks} + {transport} gather of {args.gather} blocks"
                                        + ("" if args.no_overlap else " overlapped with the next frame")
                                        if nranks > 1 else "one device")},

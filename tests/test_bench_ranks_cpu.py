@@ -113,6 +113,7 @@ def _fake_wcpt(rank, nranks, log, one_visible=False):
     m.group_unique_id = lambda: UID
     m.runtime_version = lambda: 70226015
     m.build_id = lambda: "stand-in"
+    m.KERNEL_AUTO = L.KERNEL_AUTO
     # torchrun: every process sees every GPU, so LOCAL_RANK is the device; one_visible: each sees one, its own
     m.device_count = lambda: 1 if one_visible else nranks
     m.device_pci_bus_id = lambda d: f"0000:{0x11 + 0x20 * (rank if one_visible else d):02x}:00.0"
