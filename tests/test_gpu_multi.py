@@ -494,3 +494,13 @@ def test_group_with_a_middle_root_and_presenting_toggled(gpu_ctx, kernel):
     assert info["root"] == 1 and info["frames"] == len(frames)
     ref = _context_frames(s, W, H, frames, kernel=kernel)
     assert np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32))
+
+
+def test_device_pci_bus_id_names_the_gpu(gpu_ctx):
+    """wcpt_device_pci_bus_id: the identity bench.py counts GPUs by across processes ("dddd:bb:dd.f"); a device
+    ordinal that does not exist is an error."""
+    import re
+    ident = wcpt.device_pci_bus_id(0)
+    assert re.fullmatch(r"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]", ident), ident
+    with pytest.raises(wcpt.WcptError):
+        wcpt.device_pci_bus_id(wcpt.device_count() + 7)
