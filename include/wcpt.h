@@ -37,8 +37,10 @@ extern "C" {
 
 /* 2: wcpt_counters gained ref_stack_overflow_segments / ref_stack_max; the wcpt_group_* multi-device entry points.
  * 3: groups overlap each frame's gather with the next frame's render; wcpt_group_create_ex (transports),
- *    wcpt_group_unique_id / wcpt_group_create_rank (one process per device), wcpt_group_set_option, wcpt_group_info. */
-#define WCPT_ABI_VERSION 3
+ *    wcpt_group_unique_id / wcpt_group_create_rank (one process per device), wcpt_group_set_option, wcpt_group_info.
+ * 4: WCPT_GROUP_OPTION_THREADS (each local rank's share of a frame issued from a host thread of its own);
+ *    wcpt_group_info gained issue_threads; wcpt_group_set_output reads `bytes` in every process. */
+#define WCPT_ABI_VERSION 4
 
 /* ---- error codes (VkResult-compatible where a VkResult exists) ---------------------------------- */
 #define WCPT_SUCCESS                      0
@@ -364,6 +366,12 @@ typedef struct wcpt_group wcpt_group;
 #define WCPT_GROUP_TRANSPORT_COPY 1
 #define WCPT_GROUP_UNIQUE_ID_BYTES 128   /* == sizeof(ncclUniqueId) (rccl.h NCCL_UNIQUE_ID_BYTES) */
 #define WCPT_GROUP_OPTION_OVERLAP 1
+/* How a one-process group issues a frame to its devices. 1: the caller's thread issues the first local rank's share
+ * (validation, render launch, events, transfer) while a host thread per other local rank issues that rank's share at the
+ * same time, and wcpt_group_render returns once every share is enqueued (the API stays single-threaded for the caller;
+ * threads spin ~0.2 ms between frames, then sleep). 0: the caller's thread issues every rank's share in turn. -1
+ * (default): 1 when the group's ranks span more than one device, else 0. Same device work either way. */
+#define WCPT_GROUP_OPTION_THREADS 2
 typedef struct wcpt_group_info {
     int32_t nranks;            /* ranks of the group; RCCL: ncclCommCount of this process's first communicator */
     int32_t local_ranks;       /* ranks driven by this process */
@@ -374,6 +382,8 @@ typedef struct wcpt_group_info {
     int32_t distinct_devices;  /* distinct devices among this process's ranks */
     int32_t broken;            /* 1 after a transport failure aborted the communicators */
     uint64_t frames;           /* frames rendered (and, with an output set, gathered) */
+    int32_t issue_threads;     /* host threads issuing frames beside the caller's (WCPT_GROUP_OPTION_THREADS) */
+    int32_t _pad;
 } wcpt_group_info;
 int           wcpt_group_create(const int* devices, int n, int root, wcpt_group** out);
 int           wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcpt_group** out);

@@ -413,7 +413,7 @@ typedef struct {
     const oracle_draw* draws;
     float* image;
     uint32_t W, H, y0, rows;
-    uint32_t row_begin, row_end; /* local rows */
+    uint32_t* next_row;          /* shared: the next local row to claim */
     wcpt_counters cnt;
     int overflow;
 } Job;
@@ -424,16 +424,20 @@ static void* run_job(void* arg)
     Scene S;
     S.sd = j->sd; S.materials = j->materials; S.spheres = j->spheres; S.draws = j->draws;
     S.cnt = &j->cnt; S.overflow = 0;
-    for (uint32_t ly = j->row_begin; ly < j->row_end; ly++)
+    for (;;) {
+        const uint32_t ly = __atomic_fetch_add(j->next_row, 1u, __ATOMIC_RELAXED);
+        if (ly >= j->rows) break;
         for (uint32_t x = 0; x < j->W; x++)
             shade_pixel(&S, x, j->y0 + ly, j->W, j->H, j->image + ((uint64_t)ly * j->W + x) * 4u);
+    }
     j->overflow = S.overflow;
     return NULL;
 }
 
 /*
  * Render rows [y0, y0+rows) of a W x H frame into `image` (float4[rows][W], read-modify-write like the
- * reference's imageLoad/imageStore). `threads` host threads split the rows into interleaved bands.
+ * reference's imageLoad/imageStore). `threads` host threads (at most 1024) claim rows one at a time, so rows of
+ * unequal cost balance across them (every pixel is independent, pathTracer.comp:289-323, and the counters are sums).
  * Returns 0, or WCPT_ERROR_STACK_OVERFLOW if a BVH needed more than ORACLE_STACK entries.
  */
 int oracle_render(const wcpt_scene_data* sd, const wcpt_material* materials, const wcpt_sphere* spheres,
@@ -441,17 +445,17 @@ int oracle_render(const wcpt_scene_data* sd, const wcpt_material* materials, con
                   int threads, wcpt_counters* out)
 {
     if (threads < 1) threads = 1;
-    if (threads > 256) threads = 256;
+    if (threads > 1024) threads = 1024;
     if ((uint32_t)threads > rows && rows > 0) threads = (int)rows;
     Job* jobs = (Job*)calloc((size_t)threads, sizeof(Job));
     pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
     if (!jobs || !tids) { free(jobs); free(tids); return WCPT_ERROR_OUT_OF_HOST_MEMORY; }
+    uint32_t next_row = 0;
     for (int t = 0; t < threads; t++) {
         Job* j = &jobs[t];
         j->sd = sd; j->materials = materials; j->spheres = spheres; j->draws = draws; j->image = image;
         j->W = W; j->H = H; j->y0 = y0; j->rows = rows;
-        j->row_begin = (uint32_t)(((uint64_t)rows * (uint64_t)t) / (uint64_t)threads);
-        j->row_end = (uint32_t)(((uint64_t)rows * (uint64_t)(t + 1)) / (uint64_t)threads);
+        j->next_row = &next_row;
     }
     if (threads == 1) {
         run_job(&jobs[0]);

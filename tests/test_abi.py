@@ -29,7 +29,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert wcpt.lib.wcpt_abi_version() == wcpt._lib.ABI_VERSION == 3
+    assert wcpt.lib.wcpt_abi_version() == wcpt._lib.ABI_VERSION == 4
 
 
 def test_option_and_kernel_constants_match_header():
@@ -156,7 +156,7 @@ def test_group_constants_match_header():
     fields = re.sub(r"/\*.*?\*/", "", fields, flags=re.S)
     names = re.findall(r"(?:int32_t|uint64_t)\s+(\w+);", fields)
     assert names == [n for n, _ in wcpt._lib.GroupInfo._fields_]
-    assert C.sizeof(wcpt._lib.GroupInfo) == 8 * 4 + 8
+    assert C.sizeof(wcpt._lib.GroupInfo) == 8 * 4 + 8 + 8
 
 
 def test_runtime_version_reported():

@@ -5,6 +5,7 @@ import argparse
 import multiprocessing as mproc
 import os
 import socket
+import time
 import sys
 
 import numpy as np
@@ -156,6 +157,44 @@ def test_rendezvous_skips_a_busy_port_and_a_foreign_listener():
         squat.close()
 
 
+def _abandoning_client(port):
+    """A client of rank 1 that sends its hello and closes before the hub answers (it gave up waiting)."""
+    import hashlib
+    import struct
+    from wcpt import rdzv
+    tok = hashlib.sha256(b"").digest()[:16]
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline:
+        try:
+            c = socket.create_connection(("127.0.0.1", port), timeout=1.0)
+        except OSError:
+            time.sleep(0.02)
+            continue
+        c.sendall(rdzv.MAGIC_CLIENT + tok + struct.pack("<I", 1))
+        c.close()
+        return
+    raise AssertionError("no hub")
+
+
+def test_rendezvous_ignores_a_client_that_gave_up():
+    """a client that sent its hello and closed before the hub answered must not be registered in place of
+    its own retry (the hub registers a client only after the client acknowledges the hub's answer)."""
+    port = _free_port()
+    ctx = mproc.get_context("spawn")
+    q = ctx.Queue()
+    hub = ctx.Process(target=_rdzv_worker, args=(0, 2, port, q))
+    hub.start()
+    _abandoning_client(port)                  # first in the hub's queue, gone before the answer
+    time.sleep(0.5)
+    peer = ctx.Process(target=_rdzv_worker, args=(1, 2, port, q))
+    peer.start()
+    got = dict(q.get(timeout=60)[:2] for _ in range(2))
+    for p in (hub, peer):
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert got[0] == got[1] == bytes(range(128))
+
+
 def test_watchdog_ends_a_hung_run():
     """--watchdog-s: a rank stuck past the limit (a peer died in a collective) exits with code 3 and says so, instead of
     hanging the launcher; a run that finishes in time cancels it."""
@@ -169,3 +208,25 @@ def test_watchdog_ends_a_hung_run():
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=25)
     assert p.returncode == 0
     assert bench._start_watchdog(0, {"rank": 0, "nranks": 1}) is None
+
+
+def test_cpu_baseline_threads_follow_the_plan():
+    """the CPU baseline runs the port on one thread per logical CPU the host reports
+    (BASELINE.md:21, SURVEY 8(d): all host cores), the 16-thread per-GPU share only beside it."""
+    t = bench.baseline_threads(cpu_count=256, affinity=16, quota=16.0)
+    assert t["threads"] == 256 and t["share_threads"] == 16 and t["logical_cpus"] == 256
+    assert bench.baseline_threads(cpu_count=4, affinity=4, quota=None)["share_threads"] == 4
+    assert bench.baseline_threads(cpu_count=4096, affinity=4096, quota=None)["threads"] == 1024  # the oracle's cap
+    here = bench.baseline_threads()
+    assert here["threads"] == min(os.cpu_count(), 1024)
+
+
+def test_cpu_baseline_runs_on_all_cores():
+    """The baseline leg itself on a small workload: cores = the host's logical CPUs, a positive rate, and the share
+    figure labelled beside it when the host has more than 16 CPUs."""
+    sys.path.insert(0, os.path.join(ROOT, "wc-path-tracer_amd"))
+    from wcpt import scene as wscene
+    s = wscene.generate("cornell")
+    cb = bench.cpu_baseline(s, 64, 64, 1, 1, budget_s=1.0, min_frames=2)
+    assert cb["cores"] == min(os.cpu_count(), 1024) and cb["kind"] == "port" and cb["value"] > 0
+    assert ("per_gpu_share" in cb) == (os.cpu_count() > 16)

@@ -79,6 +79,7 @@ def _fake_wcpt(rank, nranks, log, one_visible=False):
             log.append(("screen", W, H))
 
         def set_output(self, fmt, dst, n):
+            assert fmt == 0 or n > 0, "every process passes the output's byte count (wcpt.h wcpt_group_set_output)"
             log.append(("set_output", fmt, dst != 0))
 
         def render(self, sd, m, s, d):

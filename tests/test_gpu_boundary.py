@@ -280,6 +280,37 @@ def test_kernel_auto_picks_per_scene_and_renders_the_same_frames(gpu_ctx, name, 
             ctx.set_kernel(3)
 
 
+def test_kernel_choice_without_draws_is_the_megakernel(gpu_ctx):
+    """a render with no draw commands runs (and reports) the megakernel under WCPT_KERNEL_AUTO, and the
+    explicitly chosen variant otherwise -- not the variant an earlier AUTO render resolved to."""
+    import copy
+    s = get_scene("atrium")
+    spheres_only = copy.copy(get_scene("cornell"))
+    spheres_only.meshes = []
+    W, H = 32, 16
+    with wcpt.Context(0) as ctx:
+        dev = wcpt.DeviceScene(ctx, s)
+        dev2 = wcpt.DeviceScene(ctx, spheres_only)
+        ctx.create_screen(W, H)
+        ctx.set_kernel(wcpt.KERNEL_AUTO)
+        ctx.render(s.scene_data(W, H, max_bounce=2, frame=0), *dev.addresses())
+        assert ctx.last_kernel() == wcpt.KERNEL_WAVEFRONT
+        ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        ctx.render(spheres_only.scene_data(W, H, max_bounce=2, frame=0), *dev2.addresses())
+        assert ctx.last_kernel() == wcpt.KERNEL_MEGAKERNEL
+        ctx.set_kernel(wcpt.KERNEL_AUTO)
+        ctx.render(s.scene_data(W, H, max_bounce=2, frame=0), *dev.addresses())
+        assert ctx.last_kernel() == wcpt.KERNEL_WAVEFRONT
+        ctx.render(spheres_only.scene_data(W, H, max_bounce=2, frame=0), *dev2.addresses())
+        assert ctx.last_kernel() == wcpt.KERNEL_MEGAKERNEL
+        ctx.set_kernel(wcpt.KERNEL_WAVEFRONT)
+        ctx.render(spheres_only.scene_data(W, H, max_bounce=2, frame=0), *dev2.addresses())
+        assert ctx.last_kernel() == wcpt.KERNEL_WAVEFRONT
+        ctx.sync()
+        dev.free()
+        dev2.free()
+
+
 @pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
 def test_checkpoint_and_resume_progressive_accumulation(gpu_ctx, kernel):
     """Checkpoint / resume: the accumulation state is the float4 image plus renderedFramesCount. Read it

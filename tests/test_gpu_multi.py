@@ -236,7 +236,7 @@ def test_two_ranks_display_payload_gather_equals_oracle_composite(gpu_ctx, tmp_p
 COPY = wcpt._lib.GROUP_TRANSPORT_COPY
 
 
-def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4):
+def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, threads=-1):
     """Progressive frames through an n-rank COPY group on device 0: (presented frame bytes, each rank's block)."""
     with wcpt.Group([0] * n, root=0, transport=COPY) as g:
         devs = []
@@ -245,6 +245,7 @@ def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4):
             c.set_kernel(kernel)
             devs.append(wcpt.DeviceScene(c, s))
         g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 1 if overlap else 0)
+        g.set_option(wcpt._lib.GROUP_OPTION_THREADS, threads)
         g.create_screen(W, H)
         root = g.context(0)
         nbytes = W * H * PB[fmt]
@@ -262,6 +263,7 @@ def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4):
             d.free()
     assert info["frames"] == len(frames) and info["local_ranks"] == n and info["nranks"] == n
     assert info["transport"] == COPY and info["distinct_devices"] == 1 and info["broken"] == 0
+    assert info["issue_threads"] == (n - 1 if threads == 1 and n > 1 else 0)  # one device: threads off by default
     return raw, blocks
 
 
@@ -307,6 +309,60 @@ def test_group_overlapped_and_inline_gathers_agree(gpu_ctx, kernel):
     for f in frames:
         acc, _ = oracle.render_scene(s, W, H, max_bounce=3, frame=f, image=acc, threads=8)
     assert_close(_as_frame(a, wcpt._lib.PAYLOAD_RGBA32F, W, H).copy(), acc)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_group_issue_threads_present_the_same_frames(gpu_ctx, n, kernel, overlap):
+    """WCPT_GROUP_OPTION_THREADS 1: every local rank but the first issues its share of each frame from a host thread of
+    its own (at 8 ranks the caller's thread alone would spend more host time per frame than a c2 block renders in).
+    The presented frames and every rank's block equal the one-thread group's and one device's, bit for bit, over
+    progressive frames, overlapped and in line."""
+    s = get_scene("default_dielectric")
+    W, H, frames = 56, 33, tuple(range(6))
+    ref = _context_frames(s, W, H, frames, kernel=kernel, bounces=3)
+    fmt = wcpt._lib.PAYLOAD_RGBA32F
+    a, blocks = _group_frames(s, W, H, frames, n, fmt, kernel, overlap=overlap, bounces=3, threads=1)
+    b, _ = _group_frames(s, W, H, frames, n, fmt, kernel, overlap=overlap, bounces=3, threads=0)
+    assert a == b
+    assert np.array_equal(_as_frame(a, fmt, W, H).view(np.uint32), ref.view(np.uint32))
+    from wcpt.dist import row_block
+    for r, blk in enumerate(blocks):
+        y0, rows = row_block(H, n, r)
+        assert np.array_equal(blk.view(np.uint32), ref[y0:y0 + rows].view(np.uint32))
+
+
+def test_group_issue_threads_refuse_bad_arguments_atomically(gpu_ctx):
+    """With issue threads on, a frame whose rank-2 arguments are invalid is still refused before any rank renders
+    (validation stays on the caller's thread), and the group goes on bit-exactly."""
+    s = get_scene("cornell")
+    W, H = 40, 21
+    with wcpt.Group([0, 0, 0], transport=COPY) as g:
+        g.set_option(wcpt._lib.GROUP_OPTION_THREADS, 1)
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(3)]
+        g.create_screen(W, H)
+        root = g.context(0)
+        out = root.buffer_alloc(W * H * 16)
+        g.set_output(wcpt._lib.PAYLOAD_RGBA32F, root.buffer_address(out), W * H * 16)
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        g.render(s.scene_data(W, H, max_bounce=4, frame=0), *addr)
+        bad = [list(x) for x in addr]
+        bad[0][2] = 0                                   # rank 2: null material buffer
+        with pytest.raises(wcpt.WcptError) as e:
+            g.render(s.scene_data(W, H, max_bounce=4, frame=1), *bad)
+        assert e.value.code == -1000
+        info = g.info()
+        assert info["broken"] == 0 and info["frames"] == 1 and info["issue_threads"] == 2
+        for f in (1, 2):
+            g.render(s.scene_data(W, H, max_bounce=4, frame=f), *addr)
+        g.sync()
+        got = np.frombuffer(root.buffer_download(out, W * H * 16), np.float32).reshape(H, W, 4)
+        root.buffer_free(out)
+        for d in devs:
+            d.free()
+    ref = _context_frames(s, W, H, (0, 1, 2))
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
 def test_group_rank_with_bad_arguments_renders_nothing(gpu_ctx):

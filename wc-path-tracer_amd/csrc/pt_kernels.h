@@ -166,6 +166,7 @@ int context_error(wcpt_context* ctx, int code, const char* msg);
 int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                     uint64_t draws);
 int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows);
+void render_abandon(wcpt_context* ctx);
 
 } // namespace wcpt
 

@@ -34,8 +34,14 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/wcpt.h"
@@ -64,6 +70,42 @@ struct LocalRank {
     std::vector<void*> retired;              /* replaced payload buffers, freed at the next group-wide wait */
 };
 
+#if WCPT_GROUP_TIMERS
+/* tools-only build (tools/host_group_probe.py --timers): host nanoseconds per plan step kind, printed at destroy */
+struct StepTimers {
+    double ns[16] = {};
+    uint64_t n[16] = {};
+};
+StepTimers g_timers;
+thread_local bool t_worker = false; /* the issue threads' steps are not timed (g_timers is the caller thread's) */
+struct StepTimer {
+    int k;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit StepTimer(int kind) : k(kind) {}
+    ~StepTimer()
+    {
+        if (t_worker) return;
+        g_timers.ns[k] += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+        g_timers.n[k]++;
+    }
+};
+#define STEP_TIMER(kind) StepTimer step_timer_(kind)
+#else
+#define STEP_TIMER(kind) (void)0
+#endif
+
+/* A host thread that issues one local rank's share of every frame (WCPT_GROUP_OPTION_THREADS). It spins for a while
+ * after a frame (the next one usually follows within microseconds) and then sleeps on a condition variable. */
+struct Worker {
+    std::thread th;
+    std::atomic<uint64_t> go{0};         /* sequence number of the frame to issue */
+    std::atomic<bool> sleeping{false};
+    std::mutex m;
+    std::condition_variable cv;
+    size_t local = 0;                    /* index of its rank in wcpt_group::local */
+    int rc = 0;
+};
+
 } // namespace
 
 struct wcpt_group {
@@ -80,6 +122,18 @@ struct wcpt_group {
     uint64_t frames = 0;
     std::vector<wcpt::plan::RankState> plan_state; /* scratch of wcpt_group_render (no per-frame allocation) */
     std::vector<wcpt::plan::Step> steps;
+    /* WCPT_GROUP_OPTION_THREADS: -1 auto (on when this process's ranks span more than one device), 0 off, 1 on */
+    int threads = -1;
+    std::vector<std::unique_ptr<Worker>> workers; /* local ranks 1..n-1 (the caller's thread issues local rank 0) */
+    std::atomic<bool> stopping{false};
+    std::atomic<uint32_t> done{0};
+    uint64_t seq = 0;
+    /* the frame the workers issue (valid while wcpt_group_render waits for them) */
+    const wcpt_scene_data* job_scene = nullptr;
+    const uint64_t* job_m = nullptr;
+    const uint64_t* job_s = nullptr;
+    const uint64_t* job_d = nullptr;
+    bool job_exchange = false;
 };
 
 namespace {
@@ -213,6 +267,15 @@ int break_group(wcpt_group* g, int rc)
     return rc;
 }
 
+/* An error that only this process can have seen (a device failure, a check on the root's own destination) in a group
+ * whose other ranks live in other processes: those processes go on and post their part of the next frame's exchange,
+ * which this one no longer matches, so the group is broken here (its communicator aborted) rather than left to hang.
+ * In a one-process group every rank sees the same error and the group stays usable. */
+int split_refusal(wcpt_group* g, int rc)
+{
+    return (int)g->local.size() < g->nranks ? break_group(g, rc) : rc;
+}
+
 int alloc_group(int nranks, int root, int transport, wcpt_group** out)
 {
     wcpt_group* g = new (std::nothrow) wcpt_group();
@@ -232,6 +295,245 @@ int device_count()
         return 0;
     }
     return count;
+}
+
+} // namespace
+
+namespace {
+
+/* Issue the planned steps of rank `only` (-1: of every local rank, in plan order) for the frame in g->steps. Every
+ * error it returns must break the group (issue_frame does, once every issuing thread has finished). Issued from the caller's thread, or from a rank's worker thread: a rank's steps
+ * touch only that rank's context, streams, events and communicator (and, COPY transport, the root's frame through the
+ * sender's own device), so ranks issue independently; device-side order between them is the events'. */
+int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint64_t* materials, const uint64_t* spheres,
+              const uint64_t* draw_commands, bool exchange)
+{
+    const size_t nl = g->local.size();
+    const uint64_t px = exchange ? pixel_bytes(g->format) : 0;
+    auto local_index = [&](int rank) -> size_t {
+        for (size_t i = 0; i < nl; i++)
+            if (g->local[i].rank == rank) return i;
+        return 0; /* the plan names local ranks only */
+    };
+    auto stream_of = [&](LocalRank& lr, int s) {
+        return s == plan::kCommStream ? lr.comm_stream : wcpt::context_stream(lr.ctx);
+    };
+    auto block_bytes = [&](int rank) {
+        uint32_t y0 = 0, rows = 0;
+        block_of(g, rank, y0, rows);
+        return (uint64_t)g->width * rows * px;
+    };
+    auto frame_rows = [&](int rank) {
+        uint32_t y0 = 0, rows = 0;
+        block_of(g, rank, y0, rows);
+        return reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
+    };
+    /* 2-5 may fail only on a device or transport error. Once the plan has started, ranks (and, in a group of several
+     * processes, the peers posting their part of this frame's exchange) are out of step, so any failure breaks the
+     * group -- the same rule for a failing hipEventRecord / hipStreamWaitEvent / copy as for a failing render. */
+#define PHIP(expr, what)                                     \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return hip_fail(_e, (what));   \
+    } while (0)
+    bool in_group = false; /* inside ncclGroupStart: every transfer argument was fixed above, so a failure below is
+                            * the transport's, and a half-posted exchange is aborted rather than launched */
+    ncclResult_t xfer_err = ncclSuccess;
+    const char* xfer_what = "";
+    for (const plan::Step& st : g->steps) {
+        if (only >= 0 && st.rank != only) continue;
+        const size_t i = local_index(st.rank);
+        LocalRank& lr = g->local[i];
+        STEP_TIMER(st.op & 7);
+        if (in_group && st.op != plan::kSend && st.op != plan::kRecv) {
+            in_group = false;
+            const ncclResult_t e = ncclGroupEnd();
+            if (xfer_err != ncclSuccess) return (nccl_fail(xfer_err, xfer_what));
+            if (e != ncclSuccess) return (nccl_fail(e, "ncclGroupEnd"));
+        }
+        switch (st.op) {
+        case plan::kWaitSent:
+            PHIP(hipSetDevice(lr.device), "hipSetDevice");
+            PHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.sent[st.buffer], 0), "hipStreamWaitEvent(sent)");
+            break;
+        case plan::kSetOutput: {
+            const uint64_t bytes = block_bytes(lr.rank);
+            if (!lr.payload[st.buffer] || lr.payload_cap[st.buffer] < bytes)
+                return (group_error(WCPT_ERROR_INVALID_ARGUMENT,
+                                                  "rank %d: payload missing (set the output again)", lr.rank));
+            const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[st.buffer]), bytes,
+                                                  (uint32_t)g->format);
+            if (rc) return (rc);
+            break;
+        }
+        case plan::kRender: {
+            /* validated: a failure now is a device/launch failure, and the ranks are out of step */
+            const int rc = wcpt_render(lr.ctx, scene, materials[i], spheres[i], draw_commands[i]);
+            if (rc) return (rc);
+            break;
+        }
+        case plan::kRecordReady:
+            PHIP(hipSetDevice(lr.device), "hipSetDevice");
+            PHIP(hipEventRecord(lr.ready[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(ready)");
+            break;
+        case plan::kCommWaitReady:
+            PHIP(hipSetDevice(lr.device), "hipSetDevice");
+            PHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.ready[st.buffer], 0), "hipStreamWaitEvent(ready)");
+            break;
+        case plan::kSend:
+            if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
+                const LocalRank& rt = g->local[g->root_local]; /* the COPY transport is single-process */
+                PHIP(hipSetDevice(lr.device), "hipSetDevice");
+                PHIP(hipMemcpyPeerAsync(frame_rows(lr.rank), rt.device, lr.payload[st.buffer], lr.device,
+                                        block_bytes(lr.rank), stream_of(lr, st.stream)),
+                     "hipMemcpyPeerAsync(block)");
+                break;
+            }
+            /* fall through */
+        case plan::kRecv:
+            if (!in_group) {
+                const ncclResult_t e = ncclGroupStart();
+                if (e != ncclSuccess) return (nccl_fail(e, "ncclGroupStart"));
+                in_group = true;
+            }
+            if (xfer_err != ncclSuccess) break; /* skip the rest; the group is ended and aborted below */
+            if (st.op == plan::kSend) {
+                xfer_err = ncclSend(lr.payload[st.buffer], block_bytes(lr.rank), ncclUint8, st.peer, lr.comm,
+                                    stream_of(lr, st.stream));
+                xfer_what = "ncclSend";
+            } else {
+                xfer_err = ncclRecv(frame_rows(st.peer), block_bytes(st.peer), ncclUint8, st.peer, lr.comm,
+                                    stream_of(lr, st.stream));
+                xfer_what = "ncclRecv";
+            }
+            break;
+        case plan::kRecordSent:
+            PHIP(hipSetDevice(lr.device), "hipSetDevice");
+            PHIP(hipEventRecord(lr.sent[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(sent)");
+            lr.sent_pending[st.buffer] = true;
+            break;
+        default:
+            return (group_error(WCPT_ERROR_INVALID_ARGUMENT, "group plan step %d", st.op));
+        }
+    }
+    if (in_group) { /* a process holding only the root: its receives end the plan */
+        const ncclResult_t e = ncclGroupEnd();
+        if (xfer_err != ncclSuccess) return (nccl_fail(xfer_err, xfer_what));
+        if (e != ncclSuccess) return (nccl_fail(e, "ncclGroupEnd"));
+    }
+    return WCPT_SUCCESS;
+#undef PHIP
+}
+
+
+/* The worker's loop: wait for a frame (spin ~kSpinUs, then sleep), issue its rank's steps, report. */
+constexpr double kSpinUs = 200.0;
+
+void worker_main(wcpt_group* g, Worker* w)
+{
+#if WCPT_GROUP_TIMERS
+    t_worker = true;
+#endif
+    uint64_t seen = 0;
+    for (;;) {
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t spins = 0;
+        while (w->go.load(std::memory_order_seq_cst) == seen && !g->stopping.load(std::memory_order_relaxed)) {
+            __builtin_ia32_pause();
+            if ((++spins & 255u) == 0 &&
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kSpinUs) {
+                std::unique_lock<std::mutex> lk(w->m);
+                w->sleeping.store(true, std::memory_order_seq_cst);
+                w->cv.wait(lk, [&] {
+                    return w->go.load(std::memory_order_seq_cst) != seen || g->stopping.load(std::memory_order_seq_cst);
+                });
+                w->sleeping.store(false, std::memory_order_relaxed);
+            }
+        }
+        if (g->stopping.load(std::memory_order_acquire)) return;
+        seen = w->go.load(std::memory_order_acquire);
+        w->rc = run_steps(g, g->local[w->local].rank, g->job_scene, g->job_m, g->job_s, g->job_d, g->job_exchange);
+        g->done.fetch_add(1, std::memory_order_release);
+    }
+}
+
+void stop_workers(wcpt_group* g)
+{
+    if (g->workers.empty()) return;
+    g->stopping.store(true, std::memory_order_seq_cst);
+    for (auto& w : g->workers) {
+        std::lock_guard<std::mutex> lk(w->m);
+        w->cv.notify_one();
+    }
+    for (auto& w : g->workers)
+        if (w->th.joinable()) w->th.join();
+    g->workers.clear();
+    g->stopping.store(false);
+}
+
+bool use_threads(const wcpt_group* g)
+{
+    if (g->local.size() < 2 || g->threads == 0) return false;
+    if (g->threads == 1) return true;
+    for (const LocalRank& lr : g->local)
+        if (lr.device != g->local[0].device) return true;
+    return false;
+}
+
+/* Issue the planned frame: from the caller's thread alone, or with every local rank but the first issued by its own
+ * worker thread at the same time (the caller issues the first and waits until every worker has issued its share, so
+ * the call returns with the whole frame enqueued, as in the one-thread mode; nothing waits for the device). */
+int issue_frame(wcpt_group* g, const wcpt_scene_data* scene, const uint64_t* materials, const uint64_t* spheres,
+                const uint64_t* draw_commands, bool exchange)
+{
+    const size_t nl = g->local.size();
+    if (!use_threads(g)) {
+        const int rc = run_steps(g, -1, scene, materials, spheres, draw_commands, exchange);
+        if (rc) return break_group(g, rc);
+        g->frames++;
+        return WCPT_SUCCESS;
+    }
+    if (g->workers.size() != nl - 1) {
+        stop_workers(g);
+        try {
+            for (size_t i = 1; i < nl; i++) {
+                g->workers.emplace_back(new Worker());
+                Worker* w = g->workers.back().get();
+                w->local = i;
+                w->th = std::thread(worker_main, g, w);
+            }
+        } catch (...) {
+            stop_workers(g);
+            return group_error(WCPT_ERROR_OUT_OF_HOST_MEMORY, "could not start the group's issue threads");
+        }
+    }
+    g->job_scene = scene;
+    g->job_m = materials;
+    g->job_s = spheres;
+    g->job_d = draw_commands;
+    g->job_exchange = exchange;
+    g->done.store(0, std::memory_order_relaxed);
+    const uint64_t seq = ++g->seq;
+    for (auto& w : g->workers) {
+        w->go.store(seq, std::memory_order_seq_cst);
+        if (w->sleeping.load(std::memory_order_seq_cst)) {
+            std::lock_guard<std::mutex> lk(w->m);
+            w->cv.notify_one();
+        }
+    }
+    int rc = run_steps(g, g->local[0].rank, scene, materials, spheres, draw_commands, exchange);
+    const uint32_t want = (uint32_t)g->workers.size();
+    for (uint32_t spins = 0; g->done.load(std::memory_order_acquire) != want; spins++) {
+        if (spins < 4096u)
+            __builtin_ia32_pause();
+        else
+            std::this_thread::yield();
+    }
+    for (auto& w : g->workers)
+        if (!rc && w->rc) rc = w->rc;
+    if (rc) return break_group(g, rc);
+    g->frames++;
+    return WCPT_SUCCESS;
 }
 
 } // namespace
@@ -362,6 +664,20 @@ int wcpt_group_create_rank(int device, int nranks, int rank, int root, const uin
 int wcpt_group_destroy(wcpt_group* g)
 {
     if (!g) return WCPT_SUCCESS;
+    stop_workers(g);
+#if WCPT_GROUP_TIMERS
+    {
+        static const char* names[10] = {"wait_sent", "set_output", "render", "record_ready", "comm_wait_ready",
+                                        "send", "recv", "record_sent", "validate", ""};
+        std::fprintf(stderr, "group_timers ranks=%d frames=%llu", g->nranks, (unsigned long long)g->frames);
+        for (int k = 0; k < 9; k++)
+            if (g_timers.n[k])
+                std::fprintf(stderr, " %s=%.2fus/frame(%.2fus/call)", names[k],
+                             g_timers.ns[k] / 1e3 / (g->frames ? g->frames : 1), g_timers.ns[k] / 1e3 / g_timers.n[k]);
+        std::fprintf(stderr, "\n");
+        g_timers = StepTimers();
+    }
+#endif
     for (LocalRank& lr : g->local) {
         if (lr.ctx) (void)wcpt_sync(lr.ctx);
         if (lr.comm_stream) {
@@ -411,6 +727,12 @@ int wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uin
 int wcpt_group_set_option(wcpt_group* g, int option, int value)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    if (option == WCPT_GROUP_OPTION_THREADS) {
+        if (value < -1 || value > 1) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group threads %d (-1, 0, 1)", value);
+        g->threads = value;
+        if (!use_threads(g)) stop_workers(g);
+        return WCPT_SUCCESS;
+    }
     if (option != WCPT_GROUP_OPTION_OVERLAP) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "unknown group option %d", option);
     const int rc = wcpt_group_sync(g); /* the streams' queued work follows the mode it was queued with */
     if (rc) return rc;
@@ -444,6 +766,7 @@ int wcpt_group_info_get(wcpt_group* g, wcpt_group_info* out)
     out->distinct_devices = (int32_t)seen.size();
     out->broken = g->broken ? 1 : 0;
     out->frames = g->frames;
+    out->issue_threads = (int32_t)g->workers.size();
     return WCPT_SUCCESS;
 }
 
@@ -451,7 +774,7 @@ int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
     if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
-    if (width == 0 || height < (uint32_t)g->nranks)
+    if (width == 0 || height < (uint32_t)g->nranks) /* the same decision in every process */
         return group_error(WCPT_ERROR_INVALID_ARGUMENT, "%ux%u frame for %d row blocks", width, height, g->nranks);
     const uint32_t old_w = g->width, old_h = g->height;
     g->width = width;
@@ -465,17 +788,22 @@ int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
         if (rc) {
             g->width = old_w;
             g->height = old_h;
-            return rc;
+            /* a device failure here is this process's alone: its ranks keep the old frame while the other processes'
+             * take the new one, so the group cannot stay in step */
+            return split_refusal(g, rc);
         }
     }
-    if (g->format && g->root_local >= 0 && (uint64_t)width * height * pixel_bytes(g->format) > g->dst_bytes) {
+    /* every process knows the output's size (wcpt_group_set_output reads `bytes` everywhere), so this refusal is the
+     * same in all of them and leaves the group usable */
+    if (g->format && (uint64_t)width * height * pixel_bytes(g->format) > g->dst_bytes) {
         g->format = 0; /* the output no longer holds the frame: stop presenting until a new one is set */
         g->dst = g->dst_bytes = 0;
         const int rc = attach_payloads(g);
-        if (rc) return rc;
+        if (rc) return split_refusal(g, rc);
         return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group output too small for %ux%u: set a new one", width, height);
     }
-    return attach_payloads(g);
+    const int rc = attach_payloads(g);
+    return rc ? split_refusal(g, rc) : WCPT_SUCCESS;
 }
 
 int wcpt_group_set_output(wcpt_group* g, int format, uint64_t dst, uint64_t bytes)
@@ -483,23 +811,34 @@ int wcpt_group_set_output(wcpt_group* g, int format, uint64_t dst, uint64_t byte
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
     if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
     const bool holds_root = g->root_local >= 0;
-    if ((holds_root && dst == 0) || format == 0) {
+    /* Decisions on (format, bytes) and the frame size, which every process of a wcpt_group_create_rank group is given
+     * alike, are made alike everywhere and leave the group usable. Decisions only the root's process can make (its
+     * `dst`) are collective failures there: the other processes would post their part of the next exchange. */
+    const bool multi = (int)g->local.size() < g->nranks;
+    if (format == 0 || (holds_root && dst == 0)) {
         g->format = 0;
         g->dst = g->dst_bytes = 0;
-        return attach_payloads(g);
+        const int rc = attach_payloads(g);
+        if (rc) return split_refusal(g, rc);
+        /* one process: a null destination turns presenting off. Several processes: only format 0 does so everywhere;
+         * the others cannot see the root's destination and would go on sending */
+        if (format != 0 && multi)
+            return break_group(g, group_error(WCPT_ERROR_INVALID_ARGUMENT,
+                                              "group output: null destination with format %d; turn presenting off "
+                                              "with format 0 in every process", format));
+        return WCPT_SUCCESS;
     }
     if (!valid_format(format)) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "output format %d (3, 4 or 8)", format);
-    if (holds_root) {
-        if ((dst & 3u) || (format == WCPT_PAYLOAD_RGBA32F && (dst & 15u)))
-            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "misaligned group output");
-        if (g->width && (uint64_t)g->width * g->height * pixel_bytes(format) > bytes)
-            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group output of %llu bytes < %ux%u x %llu",
-                               (unsigned long long)bytes, g->width, g->height, (unsigned long long)pixel_bytes(format));
-    }
+    if (g->width && (uint64_t)g->width * g->height * pixel_bytes(format) > bytes)
+        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group output of %llu bytes < %ux%u x %llu",
+                           (unsigned long long)bytes, g->width, g->height, (unsigned long long)pixel_bytes(format));
+    if (holds_root && ((dst & 3u) || (format == WCPT_PAYLOAD_RGBA32F && (dst & 15u))))
+        return split_refusal(g, group_error(WCPT_ERROR_INVALID_ARGUMENT, "misaligned group output"));
     g->format = format;
     g->dst = holds_root ? dst : 0;
-    g->dst_bytes = holds_root ? bytes : 0;
-    return attach_payloads(g);
+    g->dst_bytes = bytes;
+    const int rc = attach_payloads(g);
+    return rc ? split_refusal(g, rc) : WCPT_SUCCESS;
 }
 
 int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_t* materials, const uint64_t* spheres,
@@ -516,9 +855,15 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
      * other ranks live in other processes, those processes still post their part of this frame's exchange; this one
      * cannot, so its communicator is aborted (the exchange fails there instead of waiting for a send that never
      * comes) and the group is unusable -- the collective contract of wcpt_group_create_rank. */
-    for (size_t i = 0; i < nl; i++) {
-        const int rc = wcpt::render_validate(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
-        if (rc) return (exchange && (int)nl < g->nranks) ? break_group(g, rc) : rc;
+    {
+        STEP_TIMER(8);
+        for (size_t i = 0; i < nl; i++) {
+            const int rc = wcpt::render_validate(g->local[i].ctx, scene, materials[i], spheres[i], draw_commands[i]);
+            if (rc) {
+                for (size_t j = 0; j < i; j++) wcpt::render_abandon(g->local[j].ctx);
+                return (exchange && (int)nl < g->nranks) ? break_group(g, rc) : rc;
+            }
+        }
     }
     /* 2-5. the frame's device operations in the order of group_plan.h (tests/test_group_plan.py checks that order on
      * a simulated device): payload reuse behind the previous transfer, renders, ready events, transfers, sent events */
@@ -529,113 +874,7 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
     }
     plan::frame_steps(g->nranks, g->root, g->overlap, exchange, g->transport == WCPT_GROUP_TRANSPORT_COPY, g->frames,
                       g->plan_state, g->steps);
-    const uint64_t px = exchange ? pixel_bytes(g->format) : 0;
-    auto local_index = [&](int rank) -> size_t {
-        for (size_t i = 0; i < nl; i++)
-            if (g->local[i].rank == rank) return i;
-        return 0; /* the plan names local ranks only */
-    };
-    auto stream_of = [&](LocalRank& lr, int s) {
-        return s == plan::kCommStream ? lr.comm_stream : wcpt::context_stream(lr.ctx);
-    };
-    auto block_bytes = [&](int rank) {
-        uint32_t y0 = 0, rows = 0;
-        block_of(g, rank, y0, rows);
-        return (uint64_t)g->width * rows * px;
-    };
-    auto frame_rows = [&](int rank) {
-        uint32_t y0 = 0, rows = 0;
-        block_of(g, rank, y0, rows);
-        return reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
-    };
-    bool in_group = false; /* inside ncclGroupStart: every transfer argument was fixed above, so a failure below is
-                            * the transport's, and a half-posted exchange is aborted rather than launched */
-    ncclResult_t xfer_err = ncclSuccess;
-    const char* xfer_what = "";
-    size_t renders = 0;
-    for (const plan::Step& st : g->steps) {
-        const size_t i = local_index(st.rank);
-        LocalRank& lr = g->local[i];
-        if (in_group && st.op != plan::kSend && st.op != plan::kRecv) {
-            in_group = false;
-            const ncclResult_t e = ncclGroupEnd();
-            if (xfer_err != ncclSuccess) return break_group(g, nccl_fail(xfer_err, xfer_what));
-            if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupEnd"));
-        }
-        switch (st.op) {
-        case plan::kWaitSent:
-            GHIP(hipSetDevice(lr.device), "hipSetDevice");
-            GHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.sent[st.buffer], 0), "hipStreamWaitEvent(sent)");
-            break;
-        case plan::kSetOutput: {
-            const uint64_t bytes = block_bytes(lr.rank);
-            if (!lr.payload[st.buffer] || lr.payload_cap[st.buffer] < bytes)
-                return group_error(WCPT_ERROR_INVALID_ARGUMENT, "rank %d: payload missing (set the output again)", lr.rank);
-            const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[st.buffer]), bytes,
-                                                  (uint32_t)g->format);
-            if (rc) return rc;
-            break;
-        }
-        case plan::kRender: {
-            /* validated: a failure now is a device/launch failure, and the ranks are out of step */
-            const int rc = wcpt_render(lr.ctx, scene, materials[i], spheres[i], draw_commands[i]);
-            if (rc) {
-                g->broken = true;
-                return rc;
-            }
-            if (++renders == nl) g->frames++;
-            break;
-        }
-        case plan::kRecordReady:
-            GHIP(hipSetDevice(lr.device), "hipSetDevice");
-            GHIP(hipEventRecord(lr.ready[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(ready)");
-            break;
-        case plan::kCommWaitReady:
-            GHIP(hipSetDevice(lr.device), "hipSetDevice");
-            GHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.ready[st.buffer], 0), "hipStreamWaitEvent(ready)");
-            break;
-        case plan::kSend:
-            if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
-                const LocalRank& rt = g->local[g->root_local]; /* the COPY transport is single-process */
-                GHIP(hipSetDevice(lr.device), "hipSetDevice");
-                GHIP(hipMemcpyPeerAsync(frame_rows(lr.rank), rt.device, lr.payload[st.buffer], lr.device,
-                                        block_bytes(lr.rank), stream_of(lr, st.stream)),
-                     "hipMemcpyPeerAsync(block)");
-                break;
-            }
-            /* fall through */
-        case plan::kRecv:
-            if (!in_group) {
-                const ncclResult_t e = ncclGroupStart();
-                if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupStart"));
-                in_group = true;
-            }
-            if (xfer_err != ncclSuccess) break; /* skip the rest; the group is ended and aborted below */
-            if (st.op == plan::kSend) {
-                xfer_err = ncclSend(lr.payload[st.buffer], block_bytes(lr.rank), ncclUint8, st.peer, lr.comm,
-                                    stream_of(lr, st.stream));
-                xfer_what = "ncclSend";
-            } else {
-                xfer_err = ncclRecv(frame_rows(st.peer), block_bytes(st.peer), ncclUint8, st.peer, lr.comm,
-                                    stream_of(lr, st.stream));
-                xfer_what = "ncclRecv";
-            }
-            break;
-        case plan::kRecordSent:
-            GHIP(hipSetDevice(lr.device), "hipSetDevice");
-            GHIP(hipEventRecord(lr.sent[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(sent)");
-            lr.sent_pending[st.buffer] = true;
-            break;
-        default:
-            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group plan step %d", st.op);
-        }
-    }
-    if (in_group) { /* a process holding only the root: its receives end the plan */
-        const ncclResult_t e = ncclGroupEnd();
-        if (xfer_err != ncclSuccess) return break_group(g, nccl_fail(xfer_err, xfer_what));
-        if (e != ncclSuccess) return break_group(g, nccl_fail(e, "ncclGroupEnd"));
-    }
-    return WCPT_SUCCESS;
+    return issue_frame(g, scene, materials, spheres, draw_commands, exchange);
 }
 
 int wcpt_group_sync(wcpt_group* g)

@@ -159,7 +159,31 @@ struct wcpt_context {
     int wf_pipes = WCPT_WF_PIPES_DEFAULT; /* WCPT_OPTION_WF_PIPES (2: c3 -2%, a c4 8-way row block -10%) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
-    uint64_t generation = 0;           /* bumped by every buffer alloc / upload */
+    uint64_t generation = 0;           /* bumped by every buffer alloc / upload / free and every option change */
+    /* Frame preparation of the last render (prepare_tri_records) and the last validation (render_validate), reused
+     * while nothing they read can have changed: the same draw-command address and count, no buffer allocated,
+     * uploaded or freed and no option changed since (ctx->generation), the draw commands read from the host copy of
+     * wcpt_buffer_upload (never from the device, which the application may write behind the runtime), and for the
+     * primary-ray records the same camera position. An unchanged frame -- progressive accumulation, a group's every
+     * rank every frame -- then does no draw-command copy, lookup, allocation or table compare. */
+    struct PrepCache {
+        bool valid = false;
+        uint64_t gen = 0, draws = 0;
+        uint32_t n = 0;
+        uint32_t origin[3] = {0, 0, 0};
+        bool pair_records = false, wf_fast = false;
+        int kernel_run = WCPT_KERNEL_MEGAKERNEL;
+    } prep;
+    struct ValidCache {
+        bool valid = false;
+        uint64_t gen = 0, draws = 0;
+        uint32_t n = 0;
+    } validated;
+    /* draw commands render_validate had to read from the device, handed to the render that follows it (one read, one
+     * host-blocking sync per frame instead of two) */
+    std::vector<wcpt_draw_command> handoff;
+    uint64_t handoff_draws = 0;
+    bool handoff_valid = false;
     std::vector<TriRecords> tri;       /* per draw command index */
     std::vector<uint64_t> tri_table;   /* host image of d_tri_table: {address, ntri} per draw */
     uint64_t* d_tri_table = nullptr;
@@ -267,17 +291,39 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
     const uint32_t n = sd.drawCommandCount;
     a.tri_records = nullptr;
     a.wf_fast = false;
-    if (n == 0) return WCPT_SUCCESS;
-    std::vector<wcpt_draw_command> dc(n);
+    if (n == 0) {
+        /* WCPT_KERNEL_AUTO with no draws: the megakernel (the rule below); an explicit choice stands */
+        ctx->kernel_run = ctx->kernel != WCPT_KERNEL_AUTO ? ctx->kernel : WCPT_KERNEL_MEGAKERNEL;
+        return WCPT_SUCCESS;
+    }
+    const bool handoff = ctx->handoff_valid && ctx->handoff_draws == draws && ctx->handoff.size() == n;
+    ctx->handoff_valid = false;
+    wcpt_context::PrepCache& pc = ctx->prep;
+    if (!handoff && pc.valid && pc.gen == ctx->generation && pc.draws == draws && pc.n == n &&
+        std::memcmp(pc.origin, sd.position, sizeof(pc.origin)) == 0) {
+        a.pair_records = pc.pair_records;
+        a.wf_fast = pc.wf_fast;
+        ctx->kernel_run = pc.kernel_run;
+        a.tri_records = ctx->d_tri_table;
+        return WCPT_SUCCESS;
+    }
+    pc.valid = false;
     const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
     uint64_t off = 0;
     Buffer* db = buffer_at(ctx, draws, off);
-    if (ctx->tri_cache && db && shadow_known(*db, off, dbytes)) {
-        std::memcpy(dc.data(), db->shadow.data() + off, dbytes);
+    const bool from_host = ctx->tri_cache && db && shadow_known(*db, off, dbytes);
+    std::vector<wcpt_draw_command> dc;
+    if (handoff) {
+        dc.swap(ctx->handoff);
     } else {
-        HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
-                                    ctx->stream), "hipMemcpyAsync(draw commands)");
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
+        dc.resize(n);
+        if (from_host) {
+            std::memcpy(dc.data(), db->shadow.data() + off, dbytes);
+        } else {
+            HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
+                                        ctx->stream), "hipMemcpyAsync(draw commands)");
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
+        }
     }
     if (ctx->tri.size() < n) ctx->tri.resize(n);
     constexpr uint64_t W = 5; /* table words per draw (pt_device.h kTriTableWords) */
@@ -442,6 +488,16 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(triangle record table)");
     }
     a.tri_records = ctx->d_tri_table;
+    if (from_host && !handoff) {
+        pc.valid = true;
+        pc.gen = ctx->generation;
+        pc.draws = draws;
+        pc.n = n;
+        std::memcpy(pc.origin, sd.position, sizeof(pc.origin));
+        pc.pair_records = a.pair_records;
+        pc.wf_fast = a.wf_fast;
+        pc.kernel_run = ctx->kernel_run;
+    }
     return WCPT_SUCCESS;
 }
 
@@ -554,6 +610,11 @@ namespace wcpt {
 hipStream_t context_stream(wcpt_context* ctx) { return ctx ? ctx->stream : nullptr; }
 int context_device(wcpt_context* ctx) { return ctx ? ctx->device : -1; }
 int context_error(wcpt_context* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
+/* A validated frame that will not be rendered (another rank's validation failed): drop its hand-off. */
+void render_abandon(wcpt_context* ctx)
+{
+    if (ctx) ctx->handoff_valid = false;
+}
 
 /* Every check wcpt_render would make before it launches anything, with no launch: the argument checks and, per draw
  * command, the index-count bound of the record build (prepare_tri_records). A group validates all its ranks first, so
@@ -566,14 +627,22 @@ int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t ma
     rc = check_render_args(ctx, scene, materials, spheres, draws, kModeRender);
     if (rc) return rc;
     const uint32_t n = scene->drawCommandCount;
+    ctx->handoff_valid = false;
     if (n == 0) return WCPT_SUCCESS;
-    std::vector<wcpt_draw_command> dc(n);
+    wcpt_context::ValidCache& vc = ctx->validated;
+    if (vc.valid && vc.gen == ctx->generation && vc.draws == draws && vc.n == n) return WCPT_SUCCESS;
+    vc.valid = false;
     const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
     uint64_t off = 0;
     Buffer* db = buffer_at(ctx, draws, off);
-    if (ctx->tri_cache && db && shadow_known(*db, off, dbytes)) {
+    const bool from_host = ctx->tri_cache && db && shadow_known(*db, off, dbytes);
+    std::vector<wcpt_draw_command>& dc = ctx->handoff;
+    dc.resize(n);
+    if (from_host) {
         std::memcpy(dc.data(), db->shadow.data() + off, dbytes);
     } else {
+        /* read from the device (the application may write draw commands behind the runtime); the render that follows
+         * takes these (prepare_tri_records), so a frame reads them once */
         HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
                                     ctx->stream), "hipMemcpyAsync(draw commands)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
@@ -588,6 +657,15 @@ int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t ma
                              dc[d].indexCount, (unsigned long long)(bi->bytes - oi), (unsigned long long)oi);
         if (ntri && (dc[d].vertexBuffer == 0 || dc[d].indexBuffer == 0))
             return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "draw command %u: null vertex/index buffer", d);
+    }
+    if (from_host) {
+        vc.valid = true;
+        vc.gen = ctx->generation;
+        vc.draws = draws;
+        vc.n = n;
+    } else {
+        ctx->handoff_draws = draws;
+        ctx->handoff_valid = true;
     }
     return WCPT_SUCCESS;
 }
@@ -735,6 +813,7 @@ int wcpt_set_kernel(wcpt_context* ctx, int variant)
     if (variant != WCPT_KERNEL_MEGAKERNEL && variant != WCPT_KERNEL_WAVEFRONT && variant != WCPT_KERNEL_AUTO)
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", variant);
     ctx->kernel = variant;
+    ctx->generation++; /* the cached frame preparation resolved the variant */
     return WCPT_SUCCESS;
 }
 
@@ -749,6 +828,7 @@ int wcpt_last_kernel(wcpt_context* ctx, int* variant)
 int wcpt_set_option(wcpt_context* ctx, int option, int value)
 {
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
+    ctx->generation++; /* options decide the cached frame preparation (record formats, layouts, the cache itself) */
     switch (option) {
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
@@ -903,6 +983,7 @@ int wcpt_buffer_free(wcpt_context* ctx, wcpt_buffer buf)
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(free)");
     if (it->second.raw) HIP_TRY(ctx, hipFree(it->second.raw), "hipFree");
     ctx->buffers.erase(it);
+    ctx->generation++;
     return WCPT_SUCCESS;
 }
 

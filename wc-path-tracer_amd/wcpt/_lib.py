@@ -86,7 +86,8 @@ GROUP_TRANSPORT_RCCL = 0
 GROUP_TRANSPORT_COPY = 1
 GROUP_UNIQUE_ID_BYTES = 128
 GROUP_OPTION_OVERLAP = 1
-ABI_VERSION = 3
+GROUP_OPTION_THREADS = 2
+ABI_VERSION = 4
 assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
 assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
 
@@ -116,7 +117,9 @@ class Camera(C.Structure):
 class GroupInfo(C.Structure):
     """wcpt_group_info (include/wcpt.h)."""
     _fields_ = [(n, C.c_int32) for n in ("nranks", "local_ranks", "first_local_rank", "root", "transport", "overlap",
-                                         "distinct_devices", "broken")] + [("frames", C.c_uint64)]
+                                         "distinct_devices", "broken")] + [("frames", C.c_uint64),
+                                                                           ("issue_threads", C.c_int32),
+                                                                           ("_pad", C.c_int32)]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

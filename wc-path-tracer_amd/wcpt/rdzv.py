@@ -25,6 +25,12 @@ import time
 
 MAGIC_CLIENT = b"WCPTRDZ1"
 MAGIC_HUB = b"WCPTRDZA"
+MAGIC_ACK = b"WCPTRDZK"
+# The hub serves connections one at a time and gives each HELLO_S to send its hello; a client waits longer than that
+# for the hub's answer, and the hub registers a client only once the client has acknowledged the answer, so a client
+# that gave up (and closed) is never registered in place of its own retry.
+HELLO_S = 5.0
+CLIENT_WAIT_S = 2 * HELLO_S
 
 
 class RendezvousError(RuntimeError):
@@ -89,7 +95,7 @@ class Rendezvous:
                     raise RendezvousError(f"rank 0: {len(self.peers)} of {world - 1} peers connected before the "
                                           f"timeout") from None
                 try:
-                    c.settimeout(5.0)
+                    c.settimeout(HELLO_S)
                     hello = _recv_exact(c, len(MAGIC_CLIENT) + len(tok) + 4)
                 except (OSError, RendezvousError):
                     c.close()
@@ -99,7 +105,13 @@ class Rendezvous:
                         not 0 < r < world or r in self.peers:
                     c.close()                          # another job, or not a rendezvous client at all
                     continue
-                c.sendall(MAGIC_HUB)
+                try:
+                    c.sendall(MAGIC_HUB)
+                    if _recv_exact(c, len(MAGIC_ACK)) != MAGIC_ACK:
+                        raise RendezvousError("bad acknowledgement")
+                except (OSError, RendezvousError):
+                    c.close()                          # the client gave up before the answer: it will retry
+                    continue
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 c.settimeout(timeout)
                 self.peers[r] = c
@@ -112,9 +124,10 @@ class Rendezvous:
                     except OSError:
                         continue
                     try:
-                        c.settimeout(2.0)
+                        c.settimeout(CLIENT_WAIT_S)
                         c.sendall(hello)
                         if _recv_exact(c, len(MAGIC_HUB)) == MAGIC_HUB:
+                            c.sendall(MAGIC_ACK)
                             c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                             c.settimeout(timeout)
                             self.hub, self.port = c, p
