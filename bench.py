@@ -394,6 +394,12 @@ def parse_args(argv=None):
     ap.add_argument("--verify", action="store_true",
                     help="the root re-renders the timed frame sequence on one device and checks the presented frame "
                          "against it bit for bit (adds 'verified' to the JSON line)")
+    ap.add_argument("--rccl-rehearsal", action="store_true",
+                    help="under torchrun on fewer GPUs than ranks: give each rank its own NCCL_HOSTID so that RCCL, "
+                         "which refuses two ranks of one communicator on one device of one host, runs the product's "
+                         "one-process-per-GPU group with its ranks on one GPU, exchanging over its network transport "
+                         "(sockets on the loopback) instead of xGMI: the same wcpt_group_create_rank / ncclSend / "
+                         "ncclRecv calls, another wire")
     ap.add_argument("--dist-backend", default="rccl", choices=["rccl", "gloo", "gloo-host", "torch-nccl"],
                     help="under torchrun: rccl (default) = the product's one-process-per-device group over RCCL, no "
                          "torch; gloo / gloo-host / torch-nccl = the torch.distributed gather (gloo rehearses N ranks "
@@ -411,10 +417,14 @@ def resolve_topology(args, env) -> dict:
         if args.devices:
             raise SystemExit("bench.py: --devices is for the one-process group (no WORLD_SIZE)")
         local = int(env.get("LOCAL_RANK", env.get("RANK", "0")))
+        if args.rccl_rehearsal and args.dist_backend != "rccl":
+            raise SystemExit("bench.py: --rccl-rehearsal rehearses the RCCL group (--dist-backend rccl)")
         return {"mode": "ranks" if args.dist_backend == "rccl" else "torch", "nranks": world,
                 "rank": int(env.get("RANK", "0")), "local_rank": local, "devices": [local]}
     if args.dist_backend != "rccl":
         raise SystemExit(f"bench.py: --dist-backend {args.dist_backend} needs a torchrun launch (WORLD_SIZE > 1)")
+    if args.rccl_rehearsal:
+        raise SystemExit("bench.py: --rccl-rehearsal needs a torchrun launch (WORLD_SIZE > 1)")
     n = 1 if args.gpus is None else args.gpus
     if n < 1:
         raise SystemExit(f"bench.py: --gpus {n}")
@@ -776,11 +786,23 @@ def _start_watchdog(seconds, topo):
     return t
 
 
+def rccl_rehearsal_env(env, rank: int):
+    """--rccl-rehearsal: RCCL detects two ranks on one device by (host hash, PCI bus id) and refuses them; a per-rank
+    NCCL_HOSTID gives each rank a host of its own, so the communicator forms and its peers talk over the network
+    transport (sockets; the loopback interface unless NCCL_SOCKET_IFNAME says otherwise, no InfiniBand). Set before
+    the first RCCL call of the process (ncclGetUniqueId / ncclCommInitRank read the environment then)."""
+    env["NCCL_HOSTID"] = f"wcpt-rehearsal-{rank}"
+    env.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    env.setdefault("NCCL_IB_DISABLE", "1")
+
+
 def main(argv=None):
     global wcpt
     args = parse_args(argv)
     topo = resolve_topology(args, os.environ)
     watchdog = _start_watchdog(args.watchdog_s, topo)
+    if args.rccl_rehearsal:
+        rccl_rehearsal_env(os.environ, topo["rank"])
     if topo["mode"] == "torch":
         import torch  # noqa: F401  (first: libwcpt.so then binds the HIP runtime torch loaded; one runtime per process)
         import torch.distributed as tdist
@@ -935,6 +957,9 @@ def main(argv=None):
             out["per_rank_block_ms"] = [b["block_ms"] for b in blocks]
             if distinct < nranks:
                 out["rehearsal"] = f"{nranks} ranks on {distinct} device(s): not a scaling measurement"
+                if args.rccl_rehearsal:
+                    out["rehearsal"] += (" (RCCL with a NCCL_HOSTID per rank: ncclCommInitRank, ncclSend / ncclRecv "
+                                         "over RCCL's socket transport instead of xGMI)")
         if spp > 1:
             # samples 1..spp-1 shade their primary segment from sample 0's Intersect record (same ray): the reference
             # executes those segments, this implementation does not (pathTracer.comp:309-310)

@@ -230,3 +230,20 @@ def test_cpu_baseline_runs_on_all_cores():
     cb = bench.cpu_baseline(s, 64, 64, 1, 1, budget_s=1.0, min_frames=2)
     assert cb["cores"] == min(os.cpu_count(), 1024) and cb["kind"] == "port" and cb["value"] > 0
     assert ("per_gpu_share" in cb) == (os.cpu_count() > 16)
+
+
+def test_rccl_rehearsal_flag_and_environment():
+    """--rccl-rehearsal is a torchrun-only mode of the RCCL group: it gives each rank its own NCCL_HOSTID (RCCL then
+    lets two ranks share one device and exchanges over sockets), on the loopback unless the host chose an interface."""
+    with pytest.raises(SystemExit):
+        _topo(["--rccl-rehearsal"])                                   # no launcher
+    with pytest.raises(SystemExit):
+        _topo(["--rccl-rehearsal", "--dist-backend", "gloo"], {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"})
+    t = _topo(["--rccl-rehearsal"], {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"})
+    assert t["mode"] == "ranks" and t["rank"] == 1
+    env = {"NCCL_SOCKET_IFNAME": "eth7"}
+    bench.rccl_rehearsal_env(env, 1)
+    assert env == {"NCCL_HOSTID": "wcpt-rehearsal-1", "NCCL_SOCKET_IFNAME": "eth7", "NCCL_IB_DISABLE": "1"}
+    env = {}
+    bench.rccl_rehearsal_env(env, 0)
+    assert env["NCCL_SOCKET_IFNAME"] == "lo" and env["NCCL_HOSTID"] == "wcpt-rehearsal-0"

@@ -22,6 +22,8 @@ if [ "${BENCH:-0}" = 1 ]; then
 fi
 if [ "${GROUP:-0}" = 1 ]; then
   run group_c2_g8copy 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport copy --verify --steps 50 --warmup 10
+  run rccl_rehearsal_c2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 bench.py --rccl-rehearsal --verify --steps 20 --warmup 5 --watchdog-s 150
+  run rccl_rehearsal_c2_n4 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29641 bench.py --rccl-rehearsal --verify --steps 20 --warmup 5 --watchdog-s 150
   run group_c2_g8copy_thr 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport copy --group-threads 1 --verify --steps 50 --warmup 10
 fi
 if [ "${BALANCE:-0}" = 1 ]; then
