@@ -81,6 +81,12 @@ def algorithmic_bytes(c: dict) -> int:
 STALE_PROFILES: list = []  # profiles refused because they were measured on another build (reported in the line)
 
 
+def _profile_key(args) -> str:
+    """The profiles/ file key of a bench line: its config, with "_orbit" for the moving camera (its own SQ / PMC passes,
+    since the frames differ: no image read, primary records rebuilt every frame)."""
+    return args.config + ("_orbit" if getattr(args, "camera", "still") == "orbit" else "")
+
+
 def _profile_json(path, args):
     """A committed profile summary (profiles/*.json) when it was measured on this config, kernel, camera and build: a
     profile that records another build id (wcpt_build_id of the library it measured) is refused, not reused."""
@@ -128,13 +134,14 @@ def roofline(args, tot, render_s, frame_s, devices=1, ranks=1) -> dict:
                             "algorithmic_gbs": round(alg_bytes / render_s / 1e9, 1),
                             "note": "cache-served: SURVEY 8(d) bytes priced at HBM cost; the scene stays in "
                                     "L1/L2/MALL, so this is not an HBM rate"}}
-    pm = _profile_json(args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json"), args)
+    key = _profile_key(args)
+    pm = _profile_json(args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_traffic_{key}.json"), args)
     traffic = None if pm is None else pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_frame"))
     r["traffic"] = traffic
     if traffic is not None:
         r["hbm_measured_gbs"] = round(traffic / render_s / 1e9, 2)
         r["hbm_measured_frac"] = round(traffic / render_s / 1e9 / (HBM_PEAK_GBS * devices), 4)
-    sq = _profile_json(os.path.join(ROOT, "profiles", f"sq_{args.config}.json"), args)
+    sq = _profile_json(os.path.join(ROOT, "profiles", f"sq_{key}.json"), args)
     bound = None if sq is None else sq.get("bound")
     if bound == "valu_issue":
         valu = sq["counters_per_launch"]["SQ_INSTS_VALU"] * sq.get("launches_per_frame", 1.0)
@@ -143,7 +150,7 @@ def roofline(args, tot, render_s, frame_s, devices=1, ranks=1) -> dict:
                 "unit": "G wave64 VALU instructions/s", "frac": round(achieved / (VALU_PEAK_GINSTR * devices), 3),
                 "source": f"SQ_INSTS_VALU {valu:.4g}/render ({sq.get('source', 'profiles')}) over the live render "
                           f"time; peak {SIMDS} SIMDs x {CLOCK_GHZ} GHz / {CYCLES_PER_VALU} cycles"}
-        ceil = _valu_mix_ceiling(args.config, getattr(args, "build_id", None))
+        ceil = _valu_mix_ceiling(key, getattr(args, "build_id", None))
         if ceil:
             # what this kernel's VALU mix can reach: each instruction class at the fastest rate measured for an
             # instruction of that class (tools/valu_peak.hip; v_add/v_mul/v_mov issue about twice as fast as v_fma)
@@ -167,8 +174,8 @@ def roofline(args, tot, render_s, frame_s, devices=1, ranks=1) -> dict:
             head["reused_primary_lines_per_frame"] = int(reused / steps)
     else:
         head = {"bound": "unprofiled", "achieved": None, "peak": None, "unit": None, "frac": None,
-                "source": f"no SQ counter pass of this build committed for {args.config} "
-                          f"(profiles/sq_{args.config}.json)"}
+                "source": f"no SQ counter pass of this build committed for {key} "
+                          f"(profiles/sq_{key}.json)"}
     if devices > 1:
         head["devices"] = devices  # every peak above is the sum over these GPUs
     if STALE_PROFILES:
@@ -714,6 +721,17 @@ class _Collective:
         elif self.td is not None:
             self.td.barrier()
 
+    def agree(self, flag: bool) -> bool:
+        """Rank 0's flag on every rank (a loop whose length one rank decides by its clock must run as many times on
+        all of them: each iteration posts a frame's exchange, and a rank that posts one more waits forever)."""
+        if self.rdzv is not None:
+            return bool(self.rdzv.broadcast(b"\x01" if flag else b"\x00")[0])
+        if self.td is not None:
+            box = [bool(flag)]
+            self.td.broadcast_object_list(box, src=0)
+            return bool(box[0])
+        return flag
+
     def gather_obj(self, obj):
         """Every rank's obj on rank 0 (list in rank order), None elsewhere."""
         if self.rdzv is not None:
@@ -831,7 +849,8 @@ def main(argv=None):
         coll = _Collective(topo, rdzv=rdzv)
 
     t_settle = time.perf_counter()
-    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+    # the settle phase's length is rank 0's clock's decision, agreed every 8 frames (each frame posts an exchange)
+    while coll.agree((time.perf_counter() - t_settle) * 1e3 < args.settle_ms):
         for _ in range(8):
             drv.render(frames(0))
         drv.sync()

@@ -336,12 +336,13 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          the group.
  *   wcpt_group_create_screen  CreateScreen/Resize for the whole frame (each rank allocates only its row block).
  *   wcpt_group_set_output  where the presented frame goes: device memory on the root device (e.g.
- *                          wcpt_buffer_device_address of a root-context buffer) of width*height*(payload bytes per
- *                          pixel), row-major, in WCPT_PAYLOAD_* format; dst == 0 turns presenting off (the ranks
- *                          keep accumulating their blocks). In a process that does not hold the root, only `format`
- *                          is read (0 = off) and must equal the root's. The root renders its own block straight into
- *                          the output; the other ranks' renders write their blocks into group-owned payload buffers
- *                          (no copy pass).
+ *                          wcpt_buffer_device_address of a root-context buffer) of `bytes` >= width*height*(payload
+ *                          bytes per pixel), row-major, in WCPT_PAYLOAD_* format; format 0 turns presenting off (the
+ *                          ranks keep accumulating their blocks), and so does dst == 0 in a one-process group. Every
+ *                          process passes the same `format` and `bytes` (a process that does not hold the root ignores
+ *                          `dst`), so each makes the same decision on them and on later resizes. The root renders its
+ *                          own block straight into the output; the other ranks' renders write their blocks into
+ *                          group-owned payload buffers (no copy pass).
  *   wcpt_group_render      Render on every rank of this process (scene by value; materials/spheres/draw_commands are
  *                          arrays of one device address per local rank, in rank order), then, with an output set,
  *                          the gather of this frame. Asynchronous, like wcpt_render. Every rank's arguments are
@@ -353,10 +354,14 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          the render streams, in line with the renders.
  *   wcpt_group_sync        waits for every local rank's renders and transfers (and reports a traversal-stack
  *                          overflow on any of them). The presented frame is complete after it.
- * Errors leave the group usable, except a transport failure inside a posted exchange, and, in a group created with
- * wcpt_group_create_rank, any wcpt_group_render error while presenting (the other processes still post their part of
- * the frame's exchange): the group then aborts its communicators and every later call but wcpt_group_destroy returns
- * WCPT_ERROR_DEVICE_LOST. The other processes' exchange for that frame does not complete; their host ends them.
+ * Errors leave the group usable, except (a) any failure once a frame's device work has started to be issued (a render
+ * launch, an event, a transfer: the ranks are then out of step), and (b), in a group created with
+ * wcpt_group_create_rank, an error that the other processes cannot have seen -- any wcpt_group_render error while
+ * presenting, a check of the root's own `dst` (alignment, a null dst with a nonzero format), a device failure in
+ * wcpt_group_create_screen / wcpt_group_set_output -- since the other processes still post their part of the next
+ * exchange. The group then aborts its communicators and every later call but wcpt_group_destroy returns
+ * WCPT_ERROR_DEVICE_LOST; the other processes' exchange does not complete, and their host ends them. Refusals made
+ * alike in every process (frame size, format, `bytes`) leave the group usable.
  * wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains an error. */
 /* The row-block split itself, for a host that runs one process per device (then wcpt_set_row_range with the
  * result): rank r of n renders rows [r*height/n, (r+1)*height/n). Host-only, no device needed. */

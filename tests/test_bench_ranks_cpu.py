@@ -7,6 +7,7 @@ import json
 import multiprocessing as mproc
 import os
 import socket
+import time
 import sys
 import types
 
@@ -17,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 UID = bytes((7 * i) % 256 for i in range(128))
 
 
-def _fake_wcpt(rank, nranks, log, one_visible=False):
+def _fake_wcpt(rank, nranks, log, one_visible=False, slow_ranks=False):
     """The slice of the wcpt package bench.py uses in its group modes, recording what it was asked to do.
     one_visible: the launcher shows each process only its own GPU (device 0 everywhere, distinct PCI ids)."""
     import wcpt._lib as L
@@ -86,6 +87,8 @@ def _fake_wcpt(rank, nranks, log, one_visible=False):
             assert len(m) == len(s) == len(d) == 1
             self.ctx.prof.append(1)
             self.frames += 1
+            if slow_ranks:
+                time.sleep(0.0005 * rank)   # the ranks' clocks see different frame times
             return 0
 
         def sync(self):
@@ -97,6 +100,7 @@ def _fake_wcpt(rank, nranks, log, one_visible=False):
 
         def close(self):
             log.append(("closed",))
+            log.append(("frames", self.frames))
 
     class DeviceScene:
         def __init__(self, ctx, scene):
@@ -124,18 +128,18 @@ def _fake_wcpt(rank, nranks, log, one_visible=False):
     return m
 
 
-def _rank_main(rank, world, port, out_dir, one_visible=False):
+def _rank_main(rank, world, port, out_dir, one_visible=False, settle_ms=0):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "wc-path-tracer_amd")]
     os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port - 1))
     import wcpt  # noqa: F401  (the real package: its scene module builds the Cornell box on the host)
     import wcpt.rdzv  # noqa: F401  (the real rendezvous, which stays registered under its name)
     log = []
-    sys.modules["wcpt"] = _fake_wcpt(rank, world, log, one_visible)
+    sys.modules["wcpt"] = _fake_wcpt(rank, world, log, one_visible, slow_ranks=settle_ms > 0)
     import bench
     out = open(os.path.join(out_dir, f"rank{rank}.out"), "w")
     sys.stdout = out
-    bench.main(["--gpus", str(world), "--config", "c1", "--steps", "3", "--warmup", "2", "--settle-ms", "0",
+    bench.main(["--gpus", str(world), "--config", "c1", "--steps", "3", "--warmup", "2", "--settle-ms", str(settle_ms),
                 "--no-cpu-baseline"])
     out.close()
     json.dump([list(x) for x in log], open(os.path.join(out_dir, f"rank{rank}.log"), "w"))
@@ -183,3 +187,21 @@ def test_bench_one_process_per_gpu_plumbing(tmp_path, world, one_visible):
         assert ["set_output", 3, r == 0] in log                      # rgb payloads; only the root names a frame
         assert (["output", 256 * 256 * 12] in log) == (r == 0)         # c1: 256x256, rgb 12 B/px, on the root
         assert ["set_output", 0, False] in log                         # presenting off for the untimed re-render
+
+
+def test_settle_phase_runs_the_same_frames_on_every_rank(tmp_path):
+    """The untimed settle phase lasts --settle-ms by a clock; each of its frames posts an exchange, so a rank that
+    rendered one batch more than the root would wait for a receive that never comes (a 4-rank RCCL rehearsal hung this
+    way). Rank 0's clock decides for all: with ranks whose frames take different times, every rank renders the same
+    number of frames."""
+    ctx = mproc.get_context("spawn")
+    port = _free_port()
+    world = 3
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, str(tmp_path), False, 40)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    counts = [[x[1] for x in json.load(open(tmp_path / f"rank{r}.log")) if x[0] == "frames"][0] for r in range(world)]
+    assert len(set(counts)) == 1 and counts[0] > 2 + 3, counts

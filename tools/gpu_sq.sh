@@ -1,19 +1,21 @@
 #!/bin/bash
-# Round 4: the counter passes bench.py's roofline is priced from, on the library that is loaded (its wcpt_build_id is
-# recorded in $OUT/build_id): kernel stats, FETCH_SIZE and WRITE_SIZE (HBM traffic), the SQ issue/stall sets and the VALU
-# class mix, for CONFIGS (default "c2 ref c3 c4"). One rocprofv3 --pmc pass per counter set, each under its own time
-# limit. Summarise with tools/r04_summaries.py on the host. EXTRA_PASSES=1 adds the instruction/scalar-cache passes.
+# The counter passes bench.py's roofline is priced from, on the library that is loaded (its wcpt_build_id is recorded in
+# $OUT/build_id): kernel stats, FETCH_SIZE and WRITE_SIZE (HBM traffic), the SQ issue/stall sets and the VALU class mix,
+# for CONFIGS (default "c2 ref c3 c4"; a "_orbit" suffix runs the config with the moving camera, bench.py --camera
+# orbit). One rocprofv3 --pmc pass per counter set, each under its own time limit. Summarise with
+# tools/profile_summaries.py on the host. EXTRA_PASSES=1 adds the instruction/scalar-cache passes.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${TAG:-r04_sq}; mkdir -p "$OUT"; export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-sq}; mkdir -p "$OUT"; export TMPDIR=/tmp
 python3 -c "import sys; sys.path.insert(0, 'wc-path-tracer_amd'); import wcpt; print(wcpt.build_id())" > "$OUT/build_id" || exit 1
 for cfg in ${CONFIGS:-c2 ref c3 c4}; do
-  B="--config $cfg --no-cpu-baseline --steps 2 --warmup 1"
+  base=${cfg%_orbit}; CAM=""; [ "$base" != "$cfg" ] && CAM="--camera orbit"
+  B="--config $base $CAM --no-cpu-baseline --steps 2 --warmup 1"
   [ "$cfg" = c4 ] && B="--config $cfg --no-cpu-baseline --steps 1 --warmup 0 --settle-ms 0"
-  # the kernel-stats run is the bench line's own command (tools/gpu_r04_session.sh: default steps and warmup, c4 20 + 3),
+  # the kernel-stats run is the bench line's own command (tools/gpu_r05_session.sh: default steps and warmup, c4 20 + 3),
   # so the rocprof average covers the same frames under the same sustained load as the bench's HIP events
   PB=""; [ "$cfg" = c4 ] && PB="--steps 20 --warmup 3"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$cfg" -o $cfg -- python3 bench.py --config $cfg --no-cpu-baseline $PB > "$OUT/prof_$cfg.log" 2>&1 || { echo "prof $cfg failed"; tail -3 "$OUT/prof_$cfg.log"; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$cfg" -o $cfg -- python3 bench.py --config $base $CAM --no-cpu-baseline $PB > "$OUT/prof_$cfg.log" 2>&1 || { echo "prof $cfg failed"; tail -3 "$OUT/prof_$cfg.log"; exit 1; }
   echo "prof $cfg ok"
   n=0
   PASSES=("FETCH_SIZE" "WRITE_SIZE" \

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--build-id", default=None, help="wcpt_build_id() of the library the passes measured")
     ap.add_argument("--config", default=None)
+    ap.add_argument("--camera", default="still", help="bench.py --camera of the passes (still | orbit)")
     ap.add_argument("--kernel-id", type=int, default=0)
     ap.add_argument("--per-frame", type=int, default=2,
                     help="dispatches of --frame-kernel per frame (wavefront: one wf_init per pipeline; "
@@ -81,6 +82,7 @@ def main():
         d["l2_hit_rate"] = out["TCC_HIT_sum"] / max(1.0, out["TCC_HIT_sum"] + out["TCC_MISS_sum"])
     if a.config:
         d["config"] = a.config
+        d["camera"] = a.camera
         d["kernel"] = a.kernel_id
     d["kernel_name_filter"] = a.kernel
     if a.build_id:

@@ -1,8 +1,10 @@
-"""Turn a tools/gpu_r04_sq.sh session (gpurun_out/<tag>) into the profile summaries bench.py prices its roofline from:
+"""Turn a tools/gpu_sq.sh session (gpurun_out/<tag>) into the profile summaries bench.py prices its roofline from:
 profiles/sq_<cfg>.json, valu_mix_<cfg>.json, pmc_traffic_<cfg>.json, each stamped with the build id the session
 measured (bench.py refuses a profile of another build) and the kernel time from the session's own kernel stats.
+A "_orbit" config (c2_orbit, ref_orbit) is the base config with the moving camera (bench.py --camera orbit); its
+summaries carry "camera": "orbit".
 
-    python tools/r04_summaries.py gpurun_out/r04_sq [--configs c2 ref c3 c4] [--out profiles] [--source "round 4 ..."]
+    python tools/profile_summaries.py gpurun_out/<tag> [--configs c2 ref c3 c4 c2_orbit] [--out profiles] [--source ..]
 """
 import argparse
 import csv
@@ -59,16 +61,19 @@ def main():
     build = open(os.path.join(a.dir, "build_id")).read().strip()
     tag = os.path.basename(os.path.normpath(a.dir))
     for cfg in a.configs:
-        kid, filt, lpf, bound, resource, frame_filters = SPEC[cfg]
+        base = cfg[:-len("_orbit")] if cfg.endswith("_orbit") else cfg
+        camera = "orbit" if base != cfg else "still"
+        kid, filt, lpf, bound, resource, frame_filters = SPEC[base]
         ms = kernel_ms(a.dir, cfg, filt)
-        src = (a.source or f"round 4 {tag}") + f" (tools/gpu_r04_sq.sh; {filt.split('<')[0]} {ms:.4f} ms avg from " \
-                                                 f"the session's kernel stats)"
+        src = (a.source or tag) + f" (tools/gpu_sq.sh; {filt.split('<')[0]} {ms:.4f} ms avg from " \
+                                  f"the session's kernel stats; camera {camera})"
         py = sys.executable
         subprocess.run([py, os.path.join(ROOT, "tools", "sq_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--kernel",
-                        filt, "--ms", str(ms), "--launches-per-frame", str(lpf), "--config", cfg, "--kernel-id",
+                        filt, "--ms", str(ms), "--launches-per-frame", str(lpf), "--config", base, "--camera", camera, "--kernel-id",
                         str(kid), "--bound", bound, "--resource", resource, "--source", src, "--build-id", build,
                         "--json", os.path.join(a.out, f"sq_{cfg}.json")], check=True, stdout=subprocess.DEVNULL)
-        pm = [py, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--config", cfg,
+        pm = [py, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--config", base,
+              "--camera", camera,
               "--kernel-id", str(kid), "--build-id", build, "--json", os.path.join(a.out, f"pmc_traffic_{cfg}.json")]
         pm += ["--kernel", frame_filters, "--frame-kernel", "wf_init<false"] if frame_filters else ["--kernel", filt]
         subprocess.run(pm, check=True, stdout=subprocess.DEVNULL)
@@ -92,7 +97,7 @@ def main():
                            f"({m['SQ_INSTS_VALU_FLOPS_FP32'] / tot:.3f} FLOPs per lane per VALU instruction: surplus "
                            f"{surplus:.3f} over one per add/mul/transcendental and two per FMA)")
         frac["other"] = 1.0 - sum(frac.values())
-        json.dump({"config": cfg, "kernel": kid, "kernel_name_filter": filt, "dispatches": n.get("SQ_INSTS_VALU_ADD_F32"),
+        json.dump({"config": base, "camera": camera, "kernel": kid, "kernel_name_filter": filt, "dispatches": n.get("SQ_INSTS_VALU_ADD_F32"),
                    "SQ_INSTS_VALU_per_launch": tot, "class_fraction": {k: round(v, 4) for k, v in frac.items()},
                    "build_id": build,
                    "source": src + "; one --pmc pass of SQ_INSTS_VALU and its classes; other = the remainder (moves, "

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--build-id", default=None, help="wcpt_build_id() of the library the passes measured")
     ap.add_argument("--config", default=None, help="bench config the passes ran (bench.py reads sq_<config>.json)")
+    ap.add_argument("--camera", default="still", help="bench.py --camera of the passes (still | orbit)")
     ap.add_argument("--kernel-id", type=int, default=None, help="wcpt kernel variant (0 megakernel, 2 wavefront)")
     ap.add_argument("--bound", default=None, choices=["valu_issue", "memory_latency"],
                     help="the binding resource bench.py's roofline prices against")
@@ -52,7 +53,7 @@ def main():
     if "SQ_THREAD_CYCLES_VALU" in m and "SQ_ACTIVE_INST_VALU" in m:
         out["lane_utilisation_valu"] = round(m["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * m["SQ_ACTIVE_INST_VALU"]), 3)
     out["launches_per_frame"] = a.launches_per_frame
-    for k in ("config", "bound", "resource", "source"):
+    for k in ("config", "camera", "bound", "resource", "source"):
         if getattr(a, k) is not None:
             out[k] = getattr(a, k)
     if a.kernel_id is not None:
