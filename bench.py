@@ -386,11 +386,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: gather each frame in line with the renders instead of overlapping it with the next "
                          "render (WCPT_GROUP_OPTION_OVERLAP 0)")
-    ap.add_argument("--group-threads", type=int, default=-1, choices=[-1, 0, 1],
+    ap.add_argument("--group-threads", type=int, default=None, choices=[-1, 0, 1],
                     help="one-process group: issue each rank's share of a frame from a host thread of its own "
-                         "(WCPT_GROUP_OPTION_THREADS; -1 = the library's choice: on when the ranks span several devices)")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "copy"],
-                    help="one-process group: RCCL send/recv (default) or hipMemcpyPeerAsync of each block")
+                         "(WCPT_GROUP_OPTION_THREADS; default: the library's, 0)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "copy", "direct"],
+                    help="one-process group: RCCL send/recv (default), hipMemcpyPeerAsync of each block, or direct: "
+                         "each rank's render writes its rows of the root's frame over xGMI (no transfer step)")
     ap.add_argument("--devices", default=None,
                     help="one-process group: device of each rank, comma-separated (default 0..N-1); a device listed "
                          "more than once rehearses N ranks on fewer GPUs (needs --transport copy)")
@@ -438,8 +439,8 @@ def resolve_topology(args, env) -> dict:
     devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
     if len(devices) != n:
         raise SystemExit(f"bench.py: --devices names {len(devices)} devices for --gpus {n}")
-    if len(set(devices)) < n and args.transport != "copy":
-        raise SystemExit("bench.py: a device listed twice needs --transport copy (RCCL: one rank per device)")
+    if len(set(devices)) < n and args.transport == "rccl":
+        raise SystemExit("bench.py: a device listed twice needs --transport copy or direct (RCCL: one rank per device)")
     return {"mode": "group", "nranks": n, "rank": 0, "local_rank": 0, "devices": devices}
 
 
@@ -492,7 +493,8 @@ class GroupBench:
         T = wcpt._lib
         self.topo, self.W, self.H = topo, W, H
         if topo["mode"] == "group":
-            transport = T.GROUP_TRANSPORT_COPY if args.transport == "copy" else T.GROUP_TRANSPORT_RCCL
+            transport = {"rccl": T.GROUP_TRANSPORT_RCCL, "copy": T.GROUP_TRANSPORT_COPY,
+                         "direct": T.GROUP_TRANSPORT_DIRECT}[args.transport]
             self.g = wcpt.Group(topo["devices"], root=0, transport=transport)
         else:
             uid = wcpt.group_unique_id() if topo["rank"] == 0 else None
@@ -514,7 +516,8 @@ class GroupBench:
                 c.set_option(T.OPTION_WF_PIPES, args.wf_pipes)
             self.devs.append(wcpt.DeviceScene(c, scene))
         self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
-        self.g.set_option(T.GROUP_OPTION_THREADS, getattr(args, "group_threads", -1))
+        if getattr(args, "group_threads", None) is not None:
+            self.g.set_option(T.GROUP_OPTION_THREADS, args.group_threads)
         self.g.create_screen(W, H)
         self.fmt, self.px = GATHER_FORMATS[args.gather]
         self.out = None
@@ -927,7 +930,7 @@ def main(argv=None):
         kind = {"group": "one process, one host thread, all ranks (wcpt_group_create_ex)",
                 "ranks": "one process per GPU (wcpt_group_create_rank, ncclCommInitRank; host rendezvous wcpt.rdzv)",
                 "torch": f"one process per GPU, torch.distributed {args.dist_backend} gather (rehearsal path)"}
-        transport = ("rccl" if info["transport"] == 0 else "copy" if info["transport"] == 1 else args.dist_backend)
+        transport = {0: "rccl", 1: "copy", 2: "direct"}.get(info["transport"], args.dist_backend)
         out = {
             "metric": BASELINE_METRIC,
             "value": round(value, 3),

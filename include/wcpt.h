@@ -320,10 +320,11 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *   wcpt_group_create      one process, one thread, devices[0..n) distinct device ordinals, RCCL transport
  *                          (ncclCommInitAll, rccl.h:236; grouped ncclSend/ncclRecv, rccl.h:700,722). `root` is the
  *                          rank that receives the frame.
- *   wcpt_group_create_ex   the same with a transport: WCPT_GROUP_TRANSPORT_RCCL, or WCPT_GROUP_TRANSPORT_COPY
+ *   wcpt_group_create_ex   the same with a transport: WCPT_GROUP_TRANSPORT_RCCL, WCPT_GROUP_TRANSPORT_COPY
  *                          (hipMemcpyPeerAsync of each block into the root's frame, on the sending device's copy
  *                          path; a device may then be listed more than once, so an N-rank group can be rehearsed on
- *                          fewer devices: every rank still has its own context, streams and payloads).
+ *                          fewer devices: every rank still has its own context, streams and payloads), or
+ *                          WCPT_GROUP_TRANSPORT_DIRECT (each render writes its block into the root's frame itself).
  *                          Status: the RCCL exchange of a group with n > 1 is UNVERIFIED on hardware here (it needs n
  *                          distinct GPUs, and the development boxes have one); the COPY transport runs the same
  *                          bookkeeping (payloads, events, overlap, error paths) and is tested with 2-4 ranks on one GPU.
@@ -369,13 +370,18 @@ int           wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_
 typedef struct wcpt_group wcpt_group;
 #define WCPT_GROUP_TRANSPORT_RCCL 0
 #define WCPT_GROUP_TRANSPORT_COPY 1
+/* One process (wcpt_group_create_ex): every sender's render writes its row block straight into the root's frame over
+ * xGMI (peer access, enabled at creation; refused when a sender's device cannot access the root's), so presenting a
+ * frame costs no transfer, event or copy: the host issues one launch per rank. A device may be listed more than once. */
+#define WCPT_GROUP_TRANSPORT_DIRECT 2
 #define WCPT_GROUP_UNIQUE_ID_BYTES 128   /* == sizeof(ncclUniqueId) (rccl.h NCCL_UNIQUE_ID_BYTES) */
 #define WCPT_GROUP_OPTION_OVERLAP 1
 /* How a one-process group issues a frame to its devices. 1: the caller's thread issues the first local rank's share
  * (validation, render launch, events, transfer) while a host thread per other local rank issues that rank's share at the
  * same time, and wcpt_group_render returns once every share is enqueued (the API stays single-threaded for the caller;
- * threads spin ~0.2 ms between frames, then sleep). 0: the caller's thread issues every rank's share in turn. -1
- * (default): 1 when the group's ranks span more than one device, else 0. Same device work either way. */
+ * threads spin ~0.2 ms between frames, then sleep). 0 (default): the caller's thread issues every rank's share in turn.
+ * -1: 1 when the group's ranks span more than one device, else 0. Same device work either way. Measured on one device
+ * (8 ranks): no gain, the HIP runtime serialises the threads' calls there. */
 #define WCPT_GROUP_OPTION_THREADS 2
 typedef struct wcpt_group_info {
     int32_t nranks;            /* ranks of the group; RCCL: ncclCommCount of this process's first communicator */

@@ -236,9 +236,10 @@ def test_two_ranks_display_payload_gather_equals_oracle_composite(gpu_ctx, tmp_p
 COPY = wcpt._lib.GROUP_TRANSPORT_COPY
 
 
-def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, threads=-1):
-    """Progressive frames through an n-rank COPY group on device 0: (presented frame bytes, each rank's block)."""
-    with wcpt.Group([0] * n, root=0, transport=COPY) as g:
+def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, threads=-1, transport=COPY, root=0):
+    """Progressive frames through an n-rank COPY (or DIRECT) group on device 0: (presented frame bytes, each rank's
+    block)."""
+    with wcpt.Group([0] * n, root=root, transport=transport) as g:
         devs = []
         for r in range(n):
             c = g.context(r)
@@ -247,22 +248,22 @@ def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, thre
         g.set_option(wcpt._lib.GROUP_OPTION_OVERLAP, 1 if overlap else 0)
         g.set_option(wcpt._lib.GROUP_OPTION_THREADS, threads)
         g.create_screen(W, H)
-        root = g.context(0)
+        rc = g.context(root)
         nbytes = W * H * PB[fmt]
-        out = root.buffer_from(np.full(nbytes // 4, -5.0, np.float32))
-        g.set_output(fmt, root.buffer_address(out), nbytes)
+        out = rc.buffer_from(np.full(nbytes // 4, -5.0, np.float32))
+        g.set_output(fmt, rc.buffer_address(out), nbytes)
         addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
         for f in frames:
             g.render(s.scene_data(W, H, max_bounce=bounces, frame=f), *addr)
         g.sync()
         info = g.info()
-        raw = root.buffer_download(out, nbytes)
+        raw = rc.buffer_download(out, nbytes)
         blocks = [g.context(r).readback() for r in range(n)]
-        root.buffer_free(out)
+        rc.buffer_free(out)
         for d in devs:
             d.free()
     assert info["frames"] == len(frames) and info["local_ranks"] == n and info["nranks"] == n
-    assert info["transport"] == COPY and info["distinct_devices"] == 1 and info["broken"] == 0
+    assert info["transport"] == transport and info["distinct_devices"] == 1 and info["broken"] == 0
     assert info["issue_threads"] == (n - 1 if threads == 1 and n > 1 else 0)  # one device: threads off by default
     return raw, blocks
 
@@ -331,6 +332,61 @@ def test_group_issue_threads_present_the_same_frames(gpu_ctx, n, kernel, overlap
     for r, blk in enumerate(blocks):
         y0, rows = row_block(H, n, r)
         assert np.array_equal(blk.view(np.uint32), ref[y0:y0 + rows].view(np.uint32))
+
+
+DIRECT = wcpt._lib.GROUP_TRANSPORT_DIRECT
+
+
+@pytest.mark.parametrize("n,root", [(2, 0), (3, 1), (8, 0)])
+@pytest.mark.parametrize("fmt", [wcpt._lib.PAYLOAD_RGB32F, wcpt._lib.PAYLOAD_RGBA32F, wcpt._lib.PAYLOAD_DISPLAY_RGBA8])
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_group_direct_transport_equals_one_device(gpu_ctx, n, root, fmt, kernel):
+    """WCPT_GROUP_TRANSPORT_DIRECT: every rank's render writes its rows of the root's frame itself (over xGMI between
+    GPUs; here all ranks share device 0), so a frame is one launch per rank with no transfer, event or copy. The
+    presented frames equal one device's bit for bit (display bytes: composite.comp of them), with any root."""
+    s = get_scene("cornell")
+    W, H, frames = 64, 37, (0, 1, 2)
+    ref = _context_frames(s, W, H, frames, kernel=kernel)
+    raw, blocks = _group_frames(s, W, H, frames, n, fmt, kernel, transport=DIRECT, root=root)
+    got = _as_frame(raw, fmt, W, H)
+    if fmt == wcpt._lib.PAYLOAD_DISPLAY_RGBA8:
+        assert np.array_equal(got, oracle.composite(ref)[1])
+    else:
+        assert np.array_equal(got.view(np.uint32), ref[..., :got.shape[2]].view(np.uint32))
+    from wcpt.dist import row_block
+    for r, blk in enumerate(blocks):
+        y0, rows = row_block(H, n, r)
+        assert np.array_equal(blk.view(np.uint32), ref[y0:y0 + rows].view(np.uint32))
+
+
+def test_group_direct_transport_across_resizes_and_outputs(gpu_ctx):
+    """DIRECT: a resize re-points every rank's rows at the frame of the new size; a new output re-points them at the new
+    buffer; presenting off and on again; each presented frame equals one device's."""
+    s = get_scene("default_dielectric")
+    with wcpt.Group([0, 0, 0], transport=DIRECT) as g:
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(3)]
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        root = g.context(0)
+        got = []
+        for (W, H) in ((40, 21), (72, 30)):
+            g.create_screen(W, H)
+            nbytes = W * H * 16
+            out = root.buffer_alloc(nbytes)
+            g.set_output(wcpt._lib.PAYLOAD_RGBA32F, root.buffer_address(out), nbytes)
+            g.render(s.scene_data(W, H, max_bounce=3, frame=0), *addr)
+            g.set_output(0, 0, 0)
+            g.render(s.scene_data(W, H, max_bounce=3, frame=1), *addr)   # accumulates, not presented
+            g.set_output(wcpt._lib.PAYLOAD_RGBA32F, root.buffer_address(out), nbytes)
+            g.render(s.scene_data(W, H, max_bounce=3, frame=2), *addr)
+            g.sync()
+            got.append((W, H, np.frombuffer(root.buffer_download(out, nbytes), np.float32).reshape(H, W, 4).copy()))
+            g.set_output(0, 0, 0)
+            root.buffer_free(out)
+        for d in devs:
+            d.free()
+    for W, H, img in got:
+        ref = _context_frames(s, W, H, (0, 1, 2), bounces=3)
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (W, H)
 
 
 def test_group_issue_threads_refuse_bad_arguments_atomically(gpu_ctx):

@@ -208,3 +208,12 @@ def test_one_process_per_rank_issues_the_same_operations(shim):
 def test_group_of_one_plans_only_renders(shim):
     steps = plan(shim, 1, 0, True, False, [0], [True] * 4)
     assert [s["op"] for s in steps] == [RENDER] * 4
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_direct_transport_plans_only_renders(shim, overlap):
+    """WCPT_GROUP_TRANSPORT_DIRECT: each sender's render writes its rows of the root's frame itself, so a frame is the
+    renders alone -- one launch per rank, nothing for the host to order between devices."""
+    n = 8
+    steps = plan(shim, n, 0, overlap, 2, list(range(n)), [True, False, True])
+    assert [(s["frame"], s["op"], s["rank"]) for s in steps] == [(f, RENDER, r) for f in range(3) for r in range(n)]

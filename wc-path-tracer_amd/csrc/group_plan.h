@@ -17,6 +17,9 @@
  *   5. sent[b] is recorded behind each sender's transfer.
  * The buffer index alternates between frames with overlap on (b = frame % 2), so frame k + 1 renders while frame k's
  * transfer is in flight; with overlap off it is always 0, and the transfer is in line with the renders.
+ * DIRECT transport: every sender's render writes its block straight into the root's frame over xGMI (its gather output
+ * is set once, at the frame's rows on the root device), so the frame is only the renders: no payload, event or
+ * transfer step, and the presented frame is complete when the renders are.
  */
 #pragma once
 
@@ -41,6 +44,9 @@ enum Op : int32_t {
 
 enum Stream : int32_t { kRenderStream = 0, kCommStream = 1 };
 
+/* wcpt.h WCPT_GROUP_TRANSPORT_* */
+enum Transport : int32_t { kRccl = 0, kCopy = 1, kDirect = 2 };
+
 struct Step {
     int32_t op, rank, buffer, peer, stream;
 };
@@ -55,10 +61,12 @@ inline int payload_buffer(bool overlap, uint64_t frame) { return overlap ? (int)
 
 /* The steps of frame `frame` for this process's ranks (`local`, in rank order), in issue order; marks sent[b] pending
  * for every sender whose transfer was planned. `exchange`: presenting with more than one rank. */
-inline void frame_steps(int nranks, int root, bool overlap, bool exchange, bool copy, uint64_t frame,
+inline void frame_steps(int nranks, int root, bool overlap, bool exchange, int transport, uint64_t frame,
                         std::vector<RankState>& local, std::vector<Step>& out)
 {
     out.clear();
+    const bool copy = transport == kCopy;
+    if (transport == kDirect) exchange = false; /* the renders are the exchange */
     const int b = payload_buffer(overlap, frame);
     if (exchange) {
         for (const RankState& lr : local) {

@@ -122,8 +122,8 @@ struct wcpt_group {
     uint64_t frames = 0;
     std::vector<wcpt::plan::RankState> plan_state; /* scratch of wcpt_group_render (no per-frame allocation) */
     std::vector<wcpt::plan::Step> steps;
-    /* WCPT_GROUP_OPTION_THREADS: -1 auto (on when this process's ranks span more than one device), 0 off, 1 on */
-    int threads = -1;
+    /* WCPT_GROUP_OPTION_THREADS: 0 off (default), 1 on, -1 on when this process's ranks span more than one device */
+    int threads = 0;
     std::vector<std::unique_ptr<Worker>> workers; /* local ranks 1..n-1 (the caller's thread issues local rank 0) */
     std::atomic<bool> stopping{false};
     std::atomic<uint32_t> done{0};
@@ -212,7 +212,8 @@ int attach_payloads(wcpt_group* g)
         uint32_t y0 = 0, rows = 0;
         block_of(g, lr.rank, y0, rows);
         const uint64_t bytes = (uint64_t)g->width * rows * pixel_bytes(g->format);
-        if (lr.rank == g->root) {
+        if (lr.rank == g->root || g->transport == WCPT_GROUP_TRANSPORT_DIRECT) {
+            /* the root renders into its rows of the frame; with the DIRECT transport every rank does, over xGMI */
             const int rc = wcpt_set_gather_output(lr.ctx, g->dst + (uint64_t)g->width * y0 * pixel_bytes(g->format),
                                                   bytes, (uint32_t)g->format);
             if (rc) return rc;
@@ -546,7 +547,8 @@ int wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcp
     *out = nullptr;
     if (!devices || n < 1) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group of %d devices", n);
     if (root < 0 || root >= n) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "root %d outside [0,%d)", root, n);
-    if (transport != WCPT_GROUP_TRANSPORT_RCCL && transport != WCPT_GROUP_TRANSPORT_COPY)
+    if (transport != WCPT_GROUP_TRANSPORT_RCCL && transport != WCPT_GROUP_TRANSPORT_COPY &&
+        transport != WCPT_GROUP_TRANSPORT_DIRECT)
         return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group transport %d", transport);
     const int count = device_count();
     if (count == 0) return group_error(WCPT_ERROR_INITIALIZATION_FAILED, "no HIP device available");
@@ -584,9 +586,9 @@ int wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcp
         }
         for (int r = 0; r < n; r++) g->local[r].comm = comms[r];
     }
-    if (n > 1 && transport == WCPT_GROUP_TRANSPORT_COPY) {
+    if (n > 1 && (transport == WCPT_GROUP_TRANSPORT_COPY || transport == WCPT_GROUP_TRANSPORT_DIRECT)) {
         /* each sender writes into the root's frame: give its device access to the root's memory (xGMI peer access
-         * where the pair supports it; otherwise hipMemcpyPeerAsync stages the copy) */
+         * where the pair supports it; otherwise, COPY only, hipMemcpyPeerAsync stages the copy) */
         for (int r = 0; r < n; r++) {
             if (r == root || devices[r] == devices[root]) continue;
             int can = 0;
@@ -597,6 +599,12 @@ int wcpt_group_create_ex(const int* devices, int n, int root, int transport, wcp
                     wcpt_group_destroy(g);
                     return hip_fail(e, "hipDeviceEnablePeerAccess");
                 }
+            } else if (transport == WCPT_GROUP_TRANSPORT_DIRECT) {
+                (void)hipGetLastError();
+                wcpt_group_destroy(g);
+                return group_error(WCPT_ERROR_INITIALIZATION_FAILED,
+                                   "DIRECT transport: device %d cannot access the root's device %d (no peer access)",
+                                   devices[r], devices[root]);
             }
             (void)hipGetLastError();
         }
@@ -872,8 +880,7 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
         g->plan_state[i].rank = g->local[i].rank;
         for (int k = 0; k < kPayloadBuffers; k++) g->plan_state[i].sent_pending[k] = g->local[i].sent_pending[k];
     }
-    plan::frame_steps(g->nranks, g->root, g->overlap, exchange, g->transport == WCPT_GROUP_TRANSPORT_COPY, g->frames,
-                      g->plan_state, g->steps);
+    plan::frame_steps(g->nranks, g->root, g->overlap, exchange, g->transport, g->frames, g->plan_state, g->steps);
     return issue_frame(g, scene, materials, spheres, draw_commands, exchange);
 }
 

@@ -84,6 +84,7 @@ COUNTER_FIELDS = WORK_FIELDS + REF_STACK_FIELDS
 # multi-device groups (wcpt_group_*)
 GROUP_TRANSPORT_RCCL = 0
 GROUP_TRANSPORT_COPY = 1
+GROUP_TRANSPORT_DIRECT = 2
 GROUP_UNIQUE_ID_BYTES = 128
 GROUP_OPTION_OVERLAP = 1
 GROUP_OPTION_THREADS = 2
