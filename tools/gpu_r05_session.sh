@@ -12,7 +12,7 @@ fi
 if [ "${HOST:-0}" = 1 ]; then
   run api_probe 120 tools/host_api_probe 4096
   run group_probe 300 python3 -u tools/host_group_probe.py --ranks 1 2 4 8 --steps 2000
-  WCPT_LIBRARY=$PWD/wc-path-tracer_amd/libwcpt_gt.so run group_probe_timers 300 python3 -u tools/host_group_probe.py --ranks 1 2 4 8 --steps 2000 --threads 0
+  WCPT_LIBRARY=$PWD/wc-path-tracer_amd/libwcpt_gt.so run group_probe_timers 300 python3 -u tools/host_group_probe.py --ranks 1 8 --steps 2000 --threads 0
 fi
 if [ "${BENCH:-0}" = 1 ]; then
   run bench_c2 600 python3 -u bench.py
@@ -20,15 +20,16 @@ if [ "${BENCH:-0}" = 1 ]; then
   [ "${BENCH_ALL:-0}" = 1 ] && run bench_c3 600 python3 -u bench.py --config c3 --no-cpu-baseline
   [ "${C4:-0}" = 1 ] && run bench_c4 900 python3 -u bench.py --config c4 --no-cpu-baseline --steps 20 --warmup 3
 fi
-if [ "${GROUP:-0}" = 1 ]; then
-  run group_c2_g8copy 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport copy --verify --steps 50 --warmup 10
-  run rccl_rehearsal_c2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 bench.py --rccl-rehearsal --verify --steps 20 --warmup 5 --watchdog-s 150
-  run rccl_rehearsal_c2_n4 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29641 bench.py --rccl-rehearsal --verify --steps 20 --warmup 5 --watchdog-s 150
-  run group_c2_g8copy_thr 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport copy --group-threads 1 --verify --steps 50 --warmup 10
-fi
 if [ "${BALANCE:-0}" = 1 ]; then
   run balance_c2 300 python3 -u tools/block_balance.py --config c2 --ns 2,4,8
   run balance_c3 300 python3 -u tools/block_balance.py --config c3 --ns 2,4,8
-  [ "${C4:-0}" = 1 ] && run balance_c4 900 python3 -u tools/block_balance.py --config c4 --ns 8
+  [ "${C4:-0}" = 1 ] && run balance_c4 900 python3 -u tools/block_balance.py --config c4 --ns 8 --frames 6 --rounds 2
+fi
+if [ "${GROUP:-0}" = 1 ]; then
+  run group_c2_g8copy 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport copy --verify --steps 50 --warmup 10
+  run group_c2_g8direct 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport direct --verify --steps 50 --warmup 10
+  run group_c2_g8copy_thr 300 python3 -u bench.py --no-cpu-baseline --gpus 8 --devices 0,0,0,0,0,0,0,0 --transport copy --group-threads 1 --verify --steps 50 --warmup 10
+  run rccl_rehearsal_c2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 bench.py --rccl-rehearsal --verify --steps 20 --warmup 5 --watchdog-s 150
+  run rccl_rehearsal_c2_n4 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29641 bench.py --rccl-rehearsal --verify --steps 20 --warmup 5 --watchdog-s 150
 fi
 echo SESSION_DONE
