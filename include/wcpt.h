@@ -325,9 +325,11 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          path; a device may then be listed more than once, so an N-rank group can be rehearsed on
  *                          fewer devices: every rank still has its own context, streams and payloads), or
  *                          WCPT_GROUP_TRANSPORT_DIRECT (each render writes its block into the root's frame itself).
- *                          Status: the RCCL exchange of a group with n > 1 is UNVERIFIED on hardware here (it needs n
- *                          distinct GPUs, and the development boxes have one); the COPY transport runs the same
- *                          bookkeeping (payloads, events, overlap, error paths) and is tested with 2-4 ranks on one GPU.
+ *                          Status: RCCL between n > 1 distinct GPUs over xGMI is UNVERIFIED on hardware here (the
+ *                          development boxes have one GPU). The one-process-per-device form (below) has run with 2
+ *                          ranks on one GPU over RCCL's socket transport (bench.py --rccl-rehearsal, frame verified
+ *                          bit-exact); the COPY and DIRECT transports run the same bookkeeping and are tested with 2-8
+ *                          ranks on one GPU.
  *   wcpt_group_unique_id / wcpt_group_create_rank   one process per device (e.g. one process per GPU under
  *                          torchrun): the root's process makes the id (ncclGetUniqueId), the host hands its 128 bytes
  *                          to every process, and each process creates its rank (ncclCommInitRank). RCCL only. All
