@@ -388,7 +388,8 @@ def parse_args(argv=None):
                          "render (WCPT_GROUP_OPTION_OVERLAP 0)")
     ap.add_argument("--group-threads", type=int, default=None, choices=[-1, 0, 1],
                     help="one-process group: issue each rank's share of a frame from a host thread of its own "
-                         "(WCPT_GROUP_OPTION_THREADS; default: the library's, 0)")
+                         "(WCPT_GROUP_OPTION_THREADS; default: the library's, -1 = on when the ranks span several "
+                         "devices)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "copy", "direct"],
                     help="one-process group: RCCL send/recv (default), hipMemcpyPeerAsync of each block, or direct: "
                          "each rank's render writes its rows of the root's frame over xGMI (no transfer step)")

@@ -20,20 +20,6 @@ if [ "${BENCH:-0}" = 1 ]; then
   [ "${BENCH_ALL:-0}" = 1 ] && run bench_c3 600 python3 -u bench.py --config c3 --no-cpu-baseline
   [ "${C4:-0}" = 1 ] && run bench_c4 900 python3 -u bench.py --config c4 --no-cpu-baseline --steps 20 --warmup 3
 fi
-if [ "${PCS:-0}" = 1 ]; then
-  # instruction-level samples of the c2 render (stochastic hardware sampling: the issuing wave's PC and its stall reason)
-  timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles \
-    --pc-sampling-interval ${PCS_INTERVAL:-1048576} --output-format csv -d "$OUT/pcs" -o pcs -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --settle-ms 50 > "$OUT/pcs.log" 2>&1
-  rc=$?; echo "pcs rc=$rc"; tail -n 5 "$OUT/pcs.log" | cut -c1-400
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit 1; fi
-  if [ $rc -eq 1 ]; then
-    timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
-      --pc-sampling-interval 1 --output-format csv -d "$OUT/pcs_ht" -o pcs -- \
-      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --settle-ms 50 > "$OUT/pcs_ht.log" 2>&1
-    rc=$?; echo "pcs host_trap rc=$rc"; tail -n 5 "$OUT/pcs_ht.log" | cut -c1-400; [ $rc -eq 0 ] || exit 1
-  fi
-fi
 if [ "${KTRACE:-0}" = 1 ]; then
   # every dispatch of a c3 135-row block (the N = 8 share) and of the full frame: per-launch durations and how the
   # pipelines' launches overlap (tools/ktrace_summary.py)

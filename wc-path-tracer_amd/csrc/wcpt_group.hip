@@ -122,8 +122,8 @@ struct wcpt_group {
     uint64_t frames = 0;
     std::vector<wcpt::plan::RankState> plan_state; /* scratch of wcpt_group_render (no per-frame allocation) */
     std::vector<wcpt::plan::Step> steps;
-    /* WCPT_GROUP_OPTION_THREADS: 0 off (default), 1 on, -1 on when this process's ranks span more than one device */
-    int threads = 0;
+    /* WCPT_GROUP_OPTION_THREADS: -1 (default) on when this process's ranks span more than one device, 0 off, 1 on */
+    int threads = -1;
     std::vector<std::unique_ptr<Worker>> workers; /* local ranks 1..n-1 (the caller's thread issues local rank 0) */
     std::atomic<bool> stopping{false};
     std::atomic<uint32_t> done{0};
