@@ -30,11 +30,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--first", action="store_true", help="rank 0's block only (a size sweep)")
     ap.add_argument("--kernel", type=int, default=-1, help="WCPT_KERNEL_* (default: bench.py's for the config)")
+    ap.add_argument("--wf-pipes", type=int, default=0, help="WCPT_OPTION_WF_PIPES (0: the library default)")
+    ap.add_argument("--skip-full", action="store_true", help="do not time the full frame (full/N columns then 0)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
     ctx = wcpt.Context(0)
     ctx.set_kernel(bench.DEFAULT_KERNEL[a.config] if a.kernel < 0 else a.kernel)
+    if a.wf_pipes:
+        ctx.set_option(wcpt._lib.OPTION_WF_PIPES, a.wf_pipes)
     dev = wcpt.DeviceScene(ctx, s)
     ctx.create_screen(W, H)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
@@ -53,14 +57,15 @@ def main():
             out.append(ms / n)
         return statistics.median(out)
 
-    full = timed(0, H)
+    full = 0.0 if a.skip_full else timed(0, H)
     print(f"{a.config}: {desc}; kernel {bench.DEFAULT_KERNEL[a.config] if a.kernel < 0 else a.kernel}; "
-          f"full frame {full:.4f} ms", flush=True)
+          f"wf pipes {a.wf_pipes or 'default'}; full frame {full:.4f} ms", flush=True)
     for n in [int(x) for x in a.ns.split(",")]:
         t = [timed(*row_block(H, n, r)) for r in range(1 if a.first else n)]
         mx, mean = max(t), sum(t) / len(t)
+        ratio = f"{mx / (full / n):.2f}" if full else "-"
         print(f"N={n}: blocks {' '.join(f'{x:.4f}' for x in t)} | max {mx:.4f} mean {mean:.4f} full/N {full / n:.4f} "
-              f"| max/(full/N) {mx / (full / n):.2f} max/mean {mx / mean:.2f}", flush=True)
+              f"| max/(full/N) {ratio} max/mean {mx / mean:.2f}", flush=True)
     dev.free()
     ctx.close()
 
