@@ -382,7 +382,8 @@ typedef struct wcpt_group wcpt_group;
  * (validation, render launch, events, transfer) while a host thread per other local rank issues that rank's share at the
  * same time, and wcpt_group_render returns once every share is enqueued (the API stays single-threaded for the caller;
  * threads spin ~0.2 ms between frames, then sleep). 0: the caller's thread issues every rank's share in turn. -1
- * (default): 1 when the group's ranks span more than one device, else 0. Same device work either way. Host issue per
+ * (default): 1 when the group's ranks span more than one device and the transport is COPY or DIRECT, else 0 (an RCCL
+ * group issues all its sends and receives inside one ncclGroupStart/End from one thread unless 1 is set). Same device work either way. Host issue per
  * frame at 8 ranks (measured on one device): COPY 95-137 us in one thread, 28-40 us with threads; DIRECT
  * 27.5 us in one thread, 13.5 us with threads. */
 #define WCPT_GROUP_OPTION_THREADS 2

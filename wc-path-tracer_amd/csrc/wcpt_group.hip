@@ -122,7 +122,8 @@ struct wcpt_group {
     uint64_t frames = 0;
     std::vector<wcpt::plan::RankState> plan_state; /* scratch of wcpt_group_render (no per-frame allocation) */
     std::vector<wcpt::plan::Step> steps;
-    /* WCPT_GROUP_OPTION_THREADS: -1 (default) on when this process's ranks span more than one device, 0 off, 1 on */
+    /* WCPT_GROUP_OPTION_THREADS: -1 (default) on when this process's ranks span more than one device (COPY, DIRECT),
+     * 0 off, 1 on */
     int threads = -1;
     std::vector<std::unique_ptr<Worker>> workers; /* local ranks 1..n-1 (the caller's thread issues local rank 0) */
     std::atomic<bool> stopping{false};
@@ -476,6 +477,10 @@ bool use_threads(const wcpt_group* g)
 {
     if (g->local.size() < 2 || g->threads == 0) return false;
     if (g->threads == 1) return true;
+    /* auto: COPY / DIRECT groups over several devices. A one-process RCCL group keeps the single-thread form (every
+     * frame's sends and receives in one ncclGroupStart/End, rccl.h:700,722) unless threads are asked for: its
+     * thread-per-device form is RCCL's other supported pattern, but no multi-GPU box here has run it. */
+    if (g->transport == WCPT_GROUP_TRANSPORT_RCCL) return false;
     for (const LocalRank& lr : g->local)
         if (lr.device != g->local[0].device) return true;
     return false;
