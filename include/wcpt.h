@@ -455,7 +455,8 @@ void     wcpt_string_free(char* text);
  * 13 = how many inputs of the block fail the fast result's class check (take the general division),
  * 14 = the two triangle acceptance forms on (u, v) = (in, in2) with t = 1 (bit 0 compares, bit 1 minimum3),
  * 15 = as 8 for the kernels' square root (sqrt_exact) against the correctly rounded sqrtf,
- * 16 = the kernels' GLSL vector / scalar on one component: in * RN(1 / in2). Host arrays of 32-bit words. */
+ * 16 = the kernels' GLSL vector / scalar on one component: in * RN(1 / in2), 17 = as 8 for the integer form of the
+ * triangle take (0 < t < rec.t as bits(t) - 1 < bits(rec.t) - 1) with rec.t = in2[i]. Host arrays of 32-bit words. */
 int      wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const uint32_t* in2,
                               uint32_t* out, uint32_t n);
 

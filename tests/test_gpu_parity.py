@@ -166,6 +166,18 @@ def test_device_acceptance_forms_agree(gpu_ctx):
     assert int((out & 1).sum()) < u.size
 
 
+def test_device_integer_take_exhaustive(gpu_ctx):
+    """The integer form of the triangle take (pt_device.h take_bits, WCPT_PAIR_ITAKE): for rec.t any positive float the
+    kernel can hold (kInfinity, the largest floats, ordinary distances, the smallest normal and denormal values, +inf),
+    `t > 0 && t < rec.t` equals `bits(t) - 1 < bits(rec.t) - 1` on ALL 2^32 t (zeros, denormals, negatives, NaNs)."""
+    rts = np.array([3.402823466e38, 3.4028233e38, np.inf, 1.0, 0.5, 2.0, 1e-3, 7.25, 123456.0, 1.1754944e-38,
+                    1.4e-45, 2.8e-45, 1e-40], np.float32)
+    hi = np.arange(65536, dtype=np.uint32)
+    for rt in rts:
+        bad = gpu_ctx.selftest(17, hi, np.full(hi.size, rt, np.float32).view(np.uint32))
+        assert int(bad.sum()) == 0, f"rec.t {rt}: the forms differ on {int(bad.sum())} t"
+
+
 def test_device_random_direction(gpu_ctx):
     x = np.arange(1000, dtype=np.uint32) * 2654435761
     out = gpu_ctx.selftest(7, x).view(np.float32).reshape(-1, 3)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5 A/B session: GPU tests (in-tree library), the parity tests on a variant library, interleaved bench A/B of
+# variants against the in-tree build (tools/gpu_libab.sh), and the c3 135-row block at 1-4 wavefront pipelines.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${TAG:-r05_ab}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
+run() { local name=$1 t=$2; shift 2; echo "=== $name $(date +%T)"; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "rc=$rc"; tail -n 3 "$OUT/$name.log" | cut -c1-500; [ $rc -eq 0 ] || exit 1; }
+if [ "${TESTS:-1}" = 1 ]; then
+  run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+fi
+for v in ${VARIANT_TESTS:-}; do
+  WCPT_LIBRARY=$PWD/wc-path-tracer_amd/variants/$v.so run pytest_gpu_$v 900 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread
+done
+if [ -n "${LIBS:-}" ]; then
+  TAG=$TAG/libab run libab 1200 bash tools/gpu_libab.sh
+fi
+if [ "${PIPES:-0}" = 1 ]; then
+  for p in 1 2 3 4; do
+    run c3_block_pipes$p 300 python3 -u tools/block_balance.py --config c3 --ns 8 --skip-full --wf-pipes $p
+  done
+  run c3_block_mk 300 python3 -u tools/block_balance.py --config c3 --ns 8 --skip-full --kernel 0
+fi
+echo SESSION_DONE

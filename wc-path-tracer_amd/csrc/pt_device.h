@@ -454,6 +454,22 @@ __device__ __forceinline__ bool accept_tri_w(float t, float u, float v, float w)
     return t > 0.0f && minimum3(u, v, w) >= 0.0f;
 }
 
+/* Integer form of the take (WCPT_PAIR_ITAKE). The reference takes an accepted triangle iff t > 0 (:132) and t < rec.t
+ * (:171). For rec.t a positive float (kInfinity at most, or an earlier accepted t > 0; never NaN), the two compares
+ * are one unsigned compare of bit patterns minus one: bits(t) - 1 < bits(rec.t) - 1. Positive floats (denormals
+ * included: IEEE compares them as nonzero) order like their bit patterns; t = +0 gives 0 - 1 = 0xFFFFFFFF, which is
+ * never below; a negative t or -0 has the sign bit, so bits - 1 >= 0x7FFFFFFF > bits(rec.t) - 1 <= 0x7F7FFFFF;
+ * a NaN t (positive 0x7F800001.. or negative) lies above every finite or infinite rec.t the same way. So the pair loop
+ * carries rec.t as rb = bits(rec.t) - 1, takes with one v_add_u32 and one v_cmp_u32 per triangle instead of two float
+ * compares and their mask AND, and converts back at the end of the leaf. The acceptance keeps its minimum3 >= 0 test
+ * (which must pass -0 and reject NaN). Device check: selftest fn 17 compares both forms on all 2^32 t against a set of
+ * rec.t values (tests/test_gpu_parity.py). */
+#ifndef WCPT_PAIR_ITAKE
+#define WCPT_PAIR_ITAKE 0
+#endif
+__device__ __forceinline__ uint32_t take_bits(float t) { return __float_as_uint(t) - 1u; }
+__device__ __forceinline__ bool accept_uvw(float u, float v, float w) { return minimum3(u, v, w) >= 0.0f; }
+
 /* pathTracer.comp:121-133 with the two edges given: e1 = b - a, e2 = c - a (:122-123); returns t or -1 */
 __device__ __forceinline__ float rayTriangleE(const Ray& r, f3 a, f3 edgeAB, f3 edgeAC)
 {
@@ -599,7 +615,12 @@ __device__ __forceinline__ PairHit rayTrianglePair(const Ray& r, const TriPair& 
     const v2f uv = u + v;
     PairHit h;
     h.t = t;
-#if WCPT_ACCEPT_MIN3
+#if WCPT_PAIR_ITAKE
+    /* t > 0 is part of the take's integer compare (take_bits) */
+    const v2f w = bc2(1.0f) - uv;
+    h.hit0 = accept_uvw(u.x, v.x, w.x);
+    h.hit1 = accept_uvw(u.y, v.y, w.y);
+#elif WCPT_ACCEPT_MIN3
     const v2f w = bc2(1.0f) - uv;
     h.hit0 = accept_tri_w(t.x, u.x, v.x, w.x);
     h.hit1 = accept_tri_w(t.y, u.y, v.y, w.y);
@@ -659,7 +680,12 @@ __device__ __forceinline__ PairHit rayTrianglePairP(const Ray& r, const TriPairP
     const v2f uv = u + v;
     PairHit h;
     h.t = t;
-#if WCPT_ACCEPT_MIN3
+#if WCPT_PAIR_ITAKE
+    /* t > 0 is part of the take's integer compare (take_bits) */
+    const v2f w = bc2(1.0f) - uv;
+    h.hit0 = accept_uvw(u.x, v.x, w.x);
+    h.hit1 = accept_uvw(u.y, v.y, w.y);
+#elif WCPT_ACCEPT_MIN3
     const v2f w = bc2(1.0f) - uv;
     h.hit0 = accept_tri_w(t.x, u.x, v.x, w.x);
     h.hit1 = accept_tri_w(t.y, u.y, v.y, w.y);
@@ -1111,6 +1137,15 @@ constexpr uint32_t kNoPeel = 0xFFFFFFFFu;
 #ifndef WCPT_PAIR_MERGE
 #define WCPT_PAIR_MERGE 0
 #endif
+#if WCPT_PAIR_ITAKE
+/* rb = bits(rec.t) - 1 (take_bits); hit0/hit1 are the acceptance without t > 0 */
+__device__ __forceinline__ void pair_take_bits(const PairHit& ph, uint32_t off, uint32_t& rb, uint32_t& tag)
+{
+    const uint32_t b0 = take_bits(ph.t.x), b1 = take_bits(ph.t.y);
+    if (ph.hit0 && b0 < rb) { rb = b0; tag = off; }
+    if (ph.hit1 && b1 < rb) { rb = b1; tag = off + 1u; }
+}
+#endif
 __device__ __forceinline__ void pair_take(const PairHit& ph, uint32_t off, float& rt, uint32_t& tag)
 {
 #if WCPT_PAIR_MERGE
@@ -1156,11 +1191,19 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         return test_at(off);
 #endif
     };
+#if WCPT_PAIR_ITAKE
+    uint32_t rb = take_bits(rt); /* rec.t as bits - 1 through the leaf (take_bits) */
+#define WCPT_TAKES(T, I) (take_bits(T) < rb)
+#define WCPT_SET_RT(T) (rb = take_bits(T))
+#else
+#define WCPT_TAKES(T, I) ((T) < rt)
+#define WCPT_SET_RT(T) (rt = (T))
+#endif
     uint32_t k = k0;
     if (k & 1u) {
         const PairHit ph = peeled_at((k >> 1) * kBytes);
         count_tri<COUNT, DIAG>(cnt);
-        if (ph.hit1 && ph.t.y < rt) { rt = ph.t.y; prim = 3u * k; }
+        if (ph.hit1 && WCPT_TAKES(ph.t.y, 1)) { WCPT_SET_RT(ph.t.y); prim = 3u * k; }
         k++;
     }
     /* whole pairs: one 32-bit byte-offset induction variable from the draw's record base, and the winner recorded
@@ -1202,7 +1245,11 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
 #endif
                 count_tri<COUNT, DIAG>(cnt);
                 count_tri<COUNT, DIAG>(cnt);
+#if WCPT_PAIR_ITAKE
+                pair_take_bits(ph, o, rb, tag);
+#else
                 pair_take(ph, o, rt, tag);
+#endif
             }
             off = offEnd;
         }
@@ -1221,15 +1268,24 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
 #endif
         count_tri<COUNT, DIAG>(cnt);
         count_tri<COUNT, DIAG>(cnt);
+#if WCPT_PAIR_ITAKE
+        pair_take_bits(ph, off, rb, tag);
+#else
         pair_take(ph, off, rt, tag);
+#endif
     }
     if (tag != kNoTag) prim = 3u * (2u * (tag / kBytes) + (tag & 1u));
     if (k < kfull) k = kfull;
     if (k < kend) {
         const PairHit ph = peeled_at((k >> 1) * kBytes);
         count_tri<COUNT, DIAG>(cnt);
-        if (ph.hit0 && ph.t.x < rt) { rt = ph.t.x; prim = 3u * k; }
+        if (ph.hit0 && WCPT_TAKES(ph.t.x, 0)) { WCPT_SET_RT(ph.t.x); prim = 3u * k; }
     }
+#if WCPT_PAIR_ITAKE
+    rt = __uint_as_float(rb + 1u);
+#endif
+#undef WCPT_TAKES
+#undef WCPT_SET_RT
 }
 
 /* Leaf (:164-178): every triangle of the leaf at index positions [curLeft, curLeft + curCount), in index order,

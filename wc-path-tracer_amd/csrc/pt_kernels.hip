@@ -350,6 +350,18 @@ __global__ __launch_bounds__(256) void pt_selftest(int fn, const uint32_t* __res
         out[i] = bad;
         break;
     }
+    case 17: { /* the take's two forms (pt_device.h take_bits) over t = (a << 16) | k, k < 2^16, for rec.t = in2: mismatches
+                  between (t > 0 && t < rec.t) and bits(t) - 1 < bits(rec.t) - 1 */
+        const float rt = __uint_as_float(in2[i]);
+        const uint32_t rb = take_bits(rt);
+        uint32_t bad = 0;
+        for (uint32_t k = 0; k < 65536u; k++) {
+            const float t = __uint_as_float((a << 16) | k);
+            bad += ((t > 0.0f && t < rt) != (take_bits(t) < rb)) ? 1u : 0u;
+        }
+        out[i] = bad;
+        break;
+    }
     case 16: { /* GLSL vector / scalar as the kernels evaluate it (pt_device.h operator/): in * RN(1 / in2) */
         const f3 q = mk3(__uint_as_float(a), 0.0f, 0.0f) / __uint_as_float(in2[i]);
         out[i] = __float_as_uint(q.x);

@@ -1228,9 +1228,9 @@ int wcpt_selftest_device(wcpt_context* ctx, int fn, const uint32_t* in, const ui
 {
     int rc = bind(ctx);
     if (rc) return rc;
-    if (!in || !out || ((fn == 6 || fn == 14 || fn == 16) && !in2))
+    if (!in || !out || ((fn == 6 || fn == 14 || fn == 16 || fn == 17) && !in2))
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "null selftest arrays");
-    if (fn < 0 || fn > 16) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
+    if (fn < 0 || fn > 17) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown selftest fn %d", fn);
     const uint64_t outw = (fn == 1) ? 4ull * n : (fn == 7 ? 3ull * n : (uint64_t)n);
     rc = ensure_scratch(ctx, (2ull * n + outw) * 4ull + 16);
     if (rc) return rc;
