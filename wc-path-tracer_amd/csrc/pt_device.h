@@ -461,12 +461,13 @@ __device__ __forceinline__ bool accept_tri_w(float t, float u, float v, float w)
  * never below; a negative t or -0 has the sign bit, so bits - 1 >= 0x7FFFFFFF > bits(rec.t) - 1 <= 0x7F7FFFFF;
  * a NaN t (positive 0x7F800001.. or negative) lies above every finite or infinite rec.t the same way. So the pair loop
  * carries rec.t as rb = bits(rec.t) - 1, takes with one v_add_u32 and one v_cmp_u32 per triangle instead of two float
- * compares and their mask AND, and converts back after the loop (the per-lane takes of peeled pairs and divergent
- * waves keep the float compares, with t > 0 moved there from the acceptance). The acceptance keeps its minimum3 >= 0 test
+ * compares and their mask AND, and converts back at the end of the leaf. The acceptance keeps its minimum3 >= 0 test
  * (which must pass -0 and reject NaN). Device check: selftest fn 17 compares both forms on all 2^32 t against a set of
- * rec.t values (tests/test_gpu_parity.py). */
+ * rec.t values (tests/test_gpu_parity.py). Measured (round 5, 6 interleaved rounds on two boxes,
+ * profiles/r05_itake_ab.log): c2 kernel 0.3635 against 0.3651 ms (-0.4 %), the reference's scene +0.3 %; the same
+ * form confined to the uniform loop gained less on c2 (-0.15 %). */
 #ifndef WCPT_PAIR_ITAKE
-#define WCPT_PAIR_ITAKE 0
+#define WCPT_PAIR_ITAKE 1
 #endif
 __device__ __forceinline__ uint32_t take_bits(float t) { return __float_as_uint(t) - 1u; }
 __device__ __forceinline__ bool accept_uvw(float u, float v, float w) { return minimum3(u, v, w) >= 0.0f; }
@@ -1192,13 +1193,14 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         return test_at(off);
 #endif
     };
-    /* the per-lane takes (peeled pairs, divergent waves): t > 0 is not part of the acceptance under WCPT_PAIR_ITAKE */
 #if WCPT_PAIR_ITAKE
-#define WCPT_TAKES(T, I) ((T) > 0.0f && (T) < rt)
+    uint32_t rb = take_bits(rt); /* rec.t as bits - 1 through the leaf (take_bits) */
+#define WCPT_TAKES(T, I) (take_bits(T) < rb)
+#define WCPT_SET_RT(T) (rb = take_bits(T))
 #else
 #define WCPT_TAKES(T, I) ((T) < rt)
-#endif
 #define WCPT_SET_RT(T) (rt = (T))
+#endif
     uint32_t k = k0;
     if (k & 1u) {
         const PairHit ph = peeled_at((k >> 1) * kBytes);
@@ -1228,10 +1230,6 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
             /* the loop counter itself in an SGPR (offU..endU): no per-lane offset arithmetic (70 -> 68 VALU per
              * pair, c2 -1.7 %). A wave-uniform loop like this one was mis-compiled inside the old nested draw loop;
              * in the flat traversal loop it is correct (tools/stack_probe.py) */
-#if WCPT_PAIR_ITAKE
-            /* rec.t as bits - 1 through the uniform loop (take_bits): one add and one unsigned compare per triangle */
-            uint32_t rb = take_bits(rt);
-#endif
             for (uint32_t o = offU; o < endU; o += kBytes) {
                 PairHit ph;
                 if constexpr (PRIM) ph = rayTrianglePairP(ray, load_pairP_const(pbase, o));
@@ -1255,9 +1253,6 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
                 pair_take(ph, o, rt, tag);
 #endif
             }
-#if WCPT_PAIR_ITAKE
-            rt = __uint_as_float(rb + 1u);
-#endif
             off = offEnd;
         }
     }
@@ -1276,8 +1271,7 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         count_tri<COUNT, DIAG>(cnt);
         count_tri<COUNT, DIAG>(cnt);
 #if WCPT_PAIR_ITAKE
-        if (ph.hit0 && ph.t.x > 0.0f && ph.t.x < rt) { rt = ph.t.x; tag = off; }
-        if (ph.hit1 && ph.t.y > 0.0f && ph.t.y < rt) { rt = ph.t.y; tag = off + 1u; }
+        pair_take_bits(ph, off, rb, tag);
 #else
         pair_take(ph, off, rt, tag);
 #endif
@@ -1289,6 +1283,9 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
         count_tri<COUNT, DIAG>(cnt);
         if (ph.hit0 && WCPT_TAKES(ph.t.x, 0)) { WCPT_SET_RT(ph.t.x); prim = 3u * k; }
     }
+#if WCPT_PAIR_ITAKE
+    rt = __uint_as_float(rb + 1u);
+#endif
 #undef WCPT_TAKES
 #undef WCPT_SET_RT
 }
