@@ -9,5 +9,19 @@ if [ "${TESTS:-1}" = 1 ]; then
   run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
   run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
-TAG=$TAG/sq CONFIGS="${CONFIGS:-c2 ref c3 c4 c2_orbit ref_orbit}" bash tools/gpu_sq.sh || exit 1
+CFGS="${CONFIGS:-c2 ref c3 c4 c2_orbit ref_orbit}"
+TAG=$TAG/sq CONFIGS="$CFGS" bash tools/gpu_sq.sh || exit 1
+# summarise on the box and drop the raw per-dispatch CSVs (gpurun copies back at most 64 MiB)
+S=$OUT/summaries; mkdir -p "$S"
+cp "$OUT/sq/build_id" "$S/build_id"
+python3 tools/profile_summaries.py "$OUT/sq" --configs $CFGS --out "$S" --source "round 5 final build ($TAG)" || exit 1
+for c in c3 c4; do
+  case " $CFGS " in *" $c "*) python3 tools/traffic_split.py "$OUT/sq/sq_$c" --json "$S/traffic_split_$c.json" > "$S/traffic_split_$c.log" || exit 1;; esac
+done
+for c in $CFGS; do
+  f=$(find "$OUT/sq/prof_$c" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" "$S/${c}_kernel_stats.csv"
+  cp "$OUT/sq/prof_$c.log" "$S/prof_$c.log" 2>/dev/null
+done
+rm -rf "$OUT"/sq/sq_* "$OUT"/sq/prof_*
+du -sh "$OUT"
 echo SESSION_DONE
