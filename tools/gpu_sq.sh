@@ -10,7 +10,10 @@ OUT=gpurun_out/${TAG:-sq}; mkdir -p "$OUT"; export TMPDIR=/tmp
 python3 -c "import sys; sys.path.insert(0, 'wc-path-tracer_amd'); import wcpt; print(wcpt.build_id())" > "$OUT/build_id" || exit 1
 for cfg in ${CONFIGS:-c2 ref c3 c4}; do
   base=${cfg%_orbit}; CAM=""; [ "$base" != "$cfg" ] && CAM="--camera orbit"
-  B="--config $base $CAM --no-cpu-baseline --steps 2 --warmup 1"
+  # the moving camera's passes skip the untimed settle phase: its frames repeat the first camera position (bench.py
+  # renders frame 0 for --settle-ms), which would otherwise make up most of the dispatches the counters average over
+  SETTLE=""; [ -n "$CAM" ] && SETTLE="--settle-ms 0 --steps 6 --warmup 0"
+  B="--config $base $CAM --no-cpu-baseline --steps 2 --warmup 1 $SETTLE"
   [ "$cfg" = c4 ] && B="--config $cfg --no-cpu-baseline --steps 1 --warmup 0 --settle-ms 0"
   # the kernel-stats run is the bench line's own command (tools/gpu_r05_session.sh: default steps and warmup, c4 20 + 3),
   # so the rocprof average covers the same frames under the same sustained load as the bench's HIP events
