@@ -19,6 +19,8 @@ if [ "${BENCH:-0}" = 1 ]; then
   [ "${BENCH_ALL:-0}" = 1 ] && run bench_ref 300 python3 -u bench.py --config ref --no-cpu-baseline
   [ "${BENCH_ALL:-0}" = 1 ] && run bench_c3 600 python3 -u bench.py --config c3 --no-cpu-baseline
   [ "${C4:-0}" = 1 ] && run bench_c4 900 python3 -u bench.py --config c4 --no-cpu-baseline --steps 20 --warmup 3
+  [ "${BENCH_ALL:-0}" = 1 ] && run bench_c2_orbit 300 python3 -u bench.py --camera orbit --no-cpu-baseline
+  [ "${BENCH_ALL:-0}" = 1 ] && run bench_ref_orbit 300 python3 -u bench.py --config ref --camera orbit --no-cpu-baseline
 fi
 if [ "${KTRACE:-0}" = 1 ]; then
   # every dispatch of a c3 135-row block (the N = 8 share) and of the full frame: per-launch durations and how the
