@@ -350,8 +350,8 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
         if (in_group && st.op != plan::kSend && st.op != plan::kRecv) {
             in_group = false;
             const ncclResult_t e = ncclGroupEnd();
-            if (xfer_err != ncclSuccess) return (nccl_fail(xfer_err, xfer_what));
-            if (e != ncclSuccess) return (nccl_fail(e, "ncclGroupEnd"));
+            if (xfer_err != ncclSuccess) return nccl_fail(xfer_err, xfer_what);
+            if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
         }
         switch (st.op) {
         case plan::kWaitSent:
@@ -361,17 +361,17 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
         case plan::kSetOutput: {
             const uint64_t bytes = block_bytes(lr.rank);
             if (!lr.payload[st.buffer] || lr.payload_cap[st.buffer] < bytes)
-                return (group_error(WCPT_ERROR_INVALID_ARGUMENT,
-                                                  "rank %d: payload missing (set the output again)", lr.rank));
+                return group_error(WCPT_ERROR_INVALID_ARGUMENT, "rank %d: payload missing (set the output again)",
+                                   lr.rank);
             const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[st.buffer]), bytes,
                                                   (uint32_t)g->format);
-            if (rc) return (rc);
+            if (rc) return rc;
             break;
         }
         case plan::kRender: {
             /* validated: a failure now is a device/launch failure, and the ranks are out of step */
             const int rc = wcpt_render(lr.ctx, scene, materials[i], spheres[i], draw_commands[i]);
-            if (rc) return (rc);
+            if (rc) return rc;
             break;
         }
         case plan::kRecordReady:
@@ -395,7 +395,7 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
         case plan::kRecv:
             if (!in_group) {
                 const ncclResult_t e = ncclGroupStart();
-                if (e != ncclSuccess) return (nccl_fail(e, "ncclGroupStart"));
+                if (e != ncclSuccess) return nccl_fail(e, "ncclGroupStart");
                 in_group = true;
             }
             if (xfer_err != ncclSuccess) break; /* skip the rest; the group is ended and aborted below */
@@ -415,18 +415,17 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
             lr.sent_pending[st.buffer] = true;
             break;
         default:
-            return (group_error(WCPT_ERROR_INVALID_ARGUMENT, "group plan step %d", st.op));
+            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group plan step %d", st.op);
         }
     }
     if (in_group) { /* a process holding only the root: its receives end the plan */
         const ncclResult_t e = ncclGroupEnd();
-        if (xfer_err != ncclSuccess) return (nccl_fail(xfer_err, xfer_what));
-        if (e != ncclSuccess) return (nccl_fail(e, "ncclGroupEnd"));
+        if (xfer_err != ncclSuccess) return nccl_fail(xfer_err, xfer_what);
+        if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
     }
     return WCPT_SUCCESS;
 #undef PHIP
 }
-
 
 /* The worker's loop: wait for a frame (spin ~kSpinUs, then sleep), issue its rank's steps, report. */
 constexpr double kSpinUs = 200.0;
