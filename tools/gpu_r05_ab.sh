@@ -14,6 +14,13 @@ done
 if [ -n "${LIBS:-}" ]; then
   TAG=$TAG/libab run libab 1200 bash tools/gpu_libab.sh
 fi
+for r in $(seq 1 ${BLOCK_ROUNDS:-0}); do
+  for v in ${BLOCK_VARIANTS:-}; do
+    if [ "$v" = cur ]; then unset WCPT_LIBRARY; else export WCPT_LIBRARY=$PWD/wc-path-tracer_amd/variants/$v.so; fi
+    run block_${BLOCK_CONFIG:-c2}_${v}_$r 300 python3 -u tools/block_balance.py --config ${BLOCK_CONFIG:-c2} --ns ${BLOCK_NS:-8} --skip-full
+    unset WCPT_LIBRARY
+  done
+done
 if [ "${PIPES:-0}" = 1 ]; then
   for p in 1 2 3 4; do
     run c3_block_pipes$p 300 python3 -u tools/block_balance.py --config c3 --ns 8 --skip-full --wf-pipes $p
