@@ -113,10 +113,6 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
 
 /* Stack kinds: 0 = private (scratch) stack of kPrivateStack entries; 1 = LDS stack of kLdsStack entries per
  * lane with a kSpillStack-entry private spill. */
-/* Wave priority by tile cost (experiment, tools/ab_build.sh): see pt_megakernel. */
-#ifndef WCPT_MK_PRIO
-#define WCPT_MK_PRIO 0
-#endif
 /* Occupancy floor for experiments (tools/ab_build.sh): __launch_bounds__'s minimum waves per SIMD. */
 #ifndef WCPT_MK_WAVES
 #define WCPT_MK_WAVES 1
@@ -136,22 +132,6 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
     const uint64_t c0 = (!COUNT && tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
     uint32_t tx, ty;
     tile_of_block(tilesX, tilesTotal, scatter, tile_order, tx, ty);
-#if WCPT_MK_PRIO
-    /* cost-ordered launch: block b renders the b-th most expensive tile, so the first quarter of the blocks are the
-     * tiles the launch's end waits for; raise their wave priority so that they win issue slots over cheaper waves
-     * sharing their SIMD (1: top quarter at 2; 2: quartiles at 3 / 2 / 1 / 0) */
-    if (!COUNT && tile_order != nullptr) {
-        const uint32_t q = (uint32_t)(((uint64_t)blockIdx.x * 4u) / tilesTotal);
-        if (q == 0u) {
-            if (WCPT_MK_PRIO == 2) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(2);
-        } else if (WCPT_MK_PRIO == 2 && q == 1u) {
-            __builtin_amdgcn_s_setprio(2);
-        } else if (WCPT_MK_PRIO == 2 && q == 2u) {
-            __builtin_amdgcn_s_setprio(1);
-        }
-    }
-#endif
     const uint32_t lx = tx * kTileW + (threadIdx.x % kTileW);
     const uint32_t ly = ty * kTileH + (threadIdx.x / kTileW);
     Counters cnt = {};
