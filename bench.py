@@ -400,6 +400,9 @@ def parse_args(argv=None):
                     help="end the process (exit 3, message on stderr) if the run has not finished after this many "
                          "seconds: a rank whose peer died, or a collective set-up that never completes, must not hang "
                          "the launcher (0 = off)")
+    ap.add_argument("--events-after", action="store_true",
+                    help="time the kernels in an untimed re-render after the timed region (as at N > 1) instead of "
+                         "with HIP events inside it (measures what the per-render event records cost)")
     ap.add_argument("--verify", action="store_true",
                     help="the root re-renders the timed frame sequence on one device and checks the presented frame "
                          "against it bit for bit (adds 'verified' to the JSON line)")
@@ -558,8 +561,9 @@ class GroupBench:
         else:
             self.g.set_output(0, 0, 0)
 
-    def profile_begin(self):
+    def profile_begin(self, region=False):
         for c in self.ctxs:
+            c.set_option(wcpt._lib.OPTION_PROFILE_REGION, 1 if region else 0)
             c.profile_begin()
 
     def profile_end(self):
@@ -685,7 +689,8 @@ class TorchBench:
         if not on:
             self.ctx.set_gather_output(0, 0)
 
-    def profile_begin(self):
+    def profile_begin(self, region=False):
+        self.ctx.set_option(wcpt._lib.OPTION_PROFILE_REGION, 1 if region else 0)
         self.ctx.profile_begin()
 
     def profile_end(self):
@@ -866,13 +871,15 @@ def main(argv=None):
         args.kernel = int(drv.ctxs[0].last_kernel())
     coll.barrier()
     drv.sync()
-    # Kernel time for the roofline: HIP events around every render on each rank's render stream. With one rank they
-    # run inside the timed region (~1 % of a c2 frame). With more they are left out of it (at 8 ranks a c2 block
-    # renders in ~0.07 ms, and two event records per render and rank are host work of that order), and the same frames
-    # are re-rendered afterwards, untimed, with the events on and presenting off.
-    live_events = nranks == 1
+    # Kernel time for the roofline. With one rank: two HIP events on the render stream bracket the timed renders
+    # (WCPT_OPTION_PROFILE_REGION), and the launch duration is their interval over the renders, the gaps between
+    # launches included; a pair of events around every render would cost ~1.3 % of a c2 frame
+    # (profiles/r05_events_ab.log). With more ranks the events are left out of the timed region (at 8 ranks a c2 block
+    # renders in ~0.07 ms, and event records per render and rank are host work of that order): the same frames are
+    # re-rendered afterwards, untimed, with a pair of events around every render and presenting off.
+    live_events = nranks == 1 and not args.events_after
     if live_events:
-        drv.profile_begin()
+        drv.profile_begin(region=True)
     t0 = time.perf_counter()
     for k in range(args.steps):
         drv.render(frames(args.warmup + k))
@@ -967,7 +974,8 @@ def main(argv=None):
             "segments_per_frame": int(segs_all / args.steps),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
             "kernel_launches_per_frame": round(sum(a["launches"] for a in allr) / max(1, len(blocks)) / args.steps, 2),
-            "kernel_timing": ("HIP events around each render on the render stream, in the timed region" if live_events
+            "kernel_timing": ("two HIP events on the render stream bracketing the timed renders: launch duration = "
+                              "their interval / renders (inter-launch gaps included)" if live_events
                               else "HIP events around each render on each rank's render stream, in an untimed "
                                    "re-render of the timed frames (N > 1: kept out of the timed steps); the slowest "
                                    "rank's average"),

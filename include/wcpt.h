@@ -106,6 +106,12 @@ extern "C" {
 /* Wavefront: concurrent pipelines (1..4, default 2). Pipeline j renders the 8x8 tiles t with t % K == j on its own
  * stream, so one pipeline's trace tail (a few slow rays) overlaps another's bulk. Same results. */
 #define WCPT_OPTION_WF_PIPES 10
+/* Kernel timing (wcpt_profile_begin / wcpt_profile_end): 0 (default) one pair of HIP events around every render;
+ * 1 two events for the whole profiled region, one before its first render and one recorded by wcpt_profile_end, so
+ * kernel_ms_total spans the renders' launches and the gaps between them, and launches counts the renders. Each event
+ * record is a packet on the stream: per-render pairs cost ~1.3 % of a 0.36-ms frame (c2: 0.3651-0.3660 against
+ * 0.3607-0.3611 ms per frame without, profiles/r05_events_ab.log). Set it outside a profiled region. */
+#define WCPT_OPTION_PROFILE_REGION 11
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

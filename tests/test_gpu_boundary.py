@@ -342,3 +342,36 @@ def test_checkpoint_and_resume_progressive_accumulation(gpu_ctx, kernel):
         resumed = b.readback()
         dev.free()
     assert np.array_equal(resumed.view(np.uint32), whole.view(np.uint32))
+
+
+def test_profile_region_times_the_renders_between_two_events(gpu_ctx):
+    """WCPT_OPTION_PROFILE_REGION: one event pair brackets every render between wcpt_profile_begin and
+    wcpt_profile_end (bench.py's N = 1 timing), launches counts the renders, and the interval covers at least the
+    per-render pairs' sum; the option is refused inside a profiled region, and 0 restores a pair per render."""
+    s = get_scene("cornell")
+    W, H = 256, 128
+    with wcpt.Context(0) as ctx:
+        dev = wcpt.DeviceScene(ctx, s)
+        ctx.create_screen(W, H)
+        sds = [s.scene_data(W, H, max_bounce=4, frame=f) for f in range(6)]
+        ctx.render(sds[0], *dev.addresses())
+        ctx.sync()
+        ctx.set_option(wcpt._lib.OPTION_PROFILE_REGION, 0)
+        ctx.profile_begin()
+        for sd in sds:
+            ctx.render(sd, *dev.addresses())
+        per_ms, per_n = ctx.profile_end()
+        ctx.set_option(wcpt._lib.OPTION_PROFILE_REGION, 1)
+        ctx.profile_begin()
+        with pytest.raises(wcpt.WcptError):
+            ctx.set_option(wcpt._lib.OPTION_PROFILE_REGION, 0)
+        for sd in sds:
+            ctx.render(sd, *dev.addresses())
+        reg_ms, reg_n = ctx.profile_end()
+        assert per_n == reg_n == len(sds)
+        assert per_ms > 0 and reg_ms > 0
+        assert reg_ms >= 0.5 * per_ms  # same renders; the region adds the gaps and drops the per-render records
+        ctx.profile_begin()  # a region with no render reports nothing
+        assert ctx.profile_end() == (0.0, 0)
+        ctx.set_option(wcpt._lib.OPTION_PROFILE_REGION, 0)
+        dev.free()

@@ -27,4 +27,10 @@ if [ "${PIPES:-0}" = 1 ]; then
   done
   run c3_block_mk 300 python3 -u tools/block_balance.py --config c3 --ns 8 --skip-full --kernel 0
 fi
+for r in $(seq 1 ${EVENT_ROUNDS:-0}); do
+  for ev in live after; do
+    if [ $ev = after ]; then A=--events-after; else A=; fi
+    run events_c2_${ev}_$r 300 python3 -u bench.py --config ${EVENT_CONFIG:-c2} --no-cpu-baseline --steps 200 $A
+  done
+done
 echo SESSION_DONE

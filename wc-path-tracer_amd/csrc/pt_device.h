@@ -989,6 +989,9 @@ struct PrivateStack {
 #ifndef WCPT_STACK_UNIFORM_FAST
 #define WCPT_STACK_UNIFORM_FAST 0
 #endif
+#ifndef WCPT_STACK_SPILL_WAIT
+#define WCPT_STACK_SPILL_WAIT 0
+#endif
 /* Entries are packed (node index | t0 bits << 32). The two storage classes are typed by address space so that
  * the compiler emits ds_read/ds_write for the LDS part and scratch_* for the spill instead of merging the two
  * into one flat access. */
@@ -1030,10 +1033,16 @@ struct LdsStack {
             e = base[sp * 64];
         } else
 #endif
-        if (sp < N)
+        if (sp < N) {
             e = base[sp * 64];
-        else
+        } else {
             e = spill[sp - N];
+#if WCPT_STACK_SPILL_WAIT
+            /* wait for the spill load inside its (rare) branch: otherwise the LDS read of the other lanes, which
+             * writes the same registers, waits for vmcnt(0) on every pop -- and so for every store still in flight */
+            __builtin_amdgcn_s_waitcnt(0x0F70); /* vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding) */
+#endif
+        }
         i = (uint32_t)e;
         t = __uint_as_float((uint32_t)(e >> 32));
     }

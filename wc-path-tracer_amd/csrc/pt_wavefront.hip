@@ -180,7 +180,13 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
  * entries run within 1%, 24 is 13% slower -- the traversal is bound by node-fetch latency, not the spill). */
 constexpr int wf_lds_per_wave(int n) { return n * 512; }
 constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
-enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3, kModeIdle = 4 };
+enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3, kModeIdle = 4, kModeIdlePend = 5 };
+/* Deferred hit stores: a lane whose ray is done keeps its (t, primitive) record in registers (kModeIdlePend, an idle
+ * lane) and the wave writes the records when it next refills, or at its exit. On gfx9 a store counts in vmcnt, and the
+ * loop's in-order vmcnt waits (the pop's, the node fetch's) would otherwise wait for it on the next iteration. */
+#ifndef WCPT_WF_DEFER_HIT
+#define WCPT_WF_DEFER_HIT 0
+#endif
 
 #ifndef WCPT_WF_TRACE_SHARE
 #define WCPT_WF_TRACE_SHARE 1
@@ -327,10 +333,14 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
     for (;;) {
         /* dynamic fetch: idle lanes take the next queued rays, once at least `refill` lanes are idle (or none
          * has work left) */
-        unsigned long long need = __ballot(mode == kModeIdle);
+        unsigned long long need = __ballot(mode >= kModeIdle);
         /* refill <= 64 (wcpt_set_option), so "every lane idle" is included in popcount >= refill; all 64 lanes stay in
          * the loop until the wave leaves it */
         if (!drained && (uint32_t)__popcll(need) >= refill) {
+            if (WCPT_WF_DEFER_HIT && mode == kModeIdlePend) {
+                b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
+                mode = kModeIdle;
+            }
             while (need) {
                 if (lo == hi) {
                     uint32_t base = 0;
@@ -384,7 +394,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             }
         }
         if (DIAG && drained && t_drain == 0) t_drain = __builtin_amdgcn_s_memtime();
-        if (!__ballot(mode != kModeIdle)) break;
+        if (!__ballot(mode < kModeIdle)) break;
         diag_mark<DIAG>(tim, tprev, 0);
         {
             const Geom& g = SINGLE ? g0 : gl;
@@ -517,13 +527,19 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             diag_mark<DIAG>(tim, tprev, 1);
             if (mode == kModeDone) {
                 /* Intersect result; wf_shade rebuilds the winner's normal and material (:204-208) */
-                b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
+                if (WCPT_WF_DEFER_HIT) {
+                    mode = kModeIdlePend;
+                } else {
+                    b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
+                    mode = kModeIdle;
+                }
                 ref_segment_end<COUNT>(cnt);
-                mode = kModeIdle;
             }
             diag_mark<DIAG>(tim, tprev, 4);
         }
     }
+    if (WCPT_WF_DEFER_HIT && mode == kModeIdlePend)
+        b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
     if (overflow) atomicOr(status, 1u);
     flush_counters<COUNT>(cnt, counters);
     if (DIAG && lane == 0) {

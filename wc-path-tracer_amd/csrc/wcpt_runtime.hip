@@ -192,6 +192,8 @@ struct wcpt_context {
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     size_t events_used = 0;
+    int profile_region = 0;     /* WCPT_OPTION_PROFILE_REGION */
+    uint32_t region_renders = 0; /* renders since wcpt_profile_begin (region timing) */
 };
 
 namespace {
@@ -556,7 +558,19 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
 #ifndef WCPT_PROFILE_EVENT_FLAGS
 #define WCPT_PROFILE_EVENT_FLAGS hipEventDisableSystemFence
 #endif
-    if (ctx->profiling && mode == wcpt::kModeRender) {
+    if (ctx->profiling && mode == wcpt::kModeRender && ctx->profile_region) {
+        /* region timing: one event before the first render; wcpt_profile_end records the closing one */
+        if (ctx->events.empty()) {
+            hipEvent_t b, c;
+            HIP_TRY(ctx, hipEventCreateWithFlags(&b, WCPT_PROFILE_EVENT_FLAGS), "hipEventCreate");
+            HIP_TRY(ctx, hipEventCreateWithFlags(&c, WCPT_PROFILE_EVENT_FLAGS), "hipEventCreate");
+            ctx->events.emplace_back(b, c);
+        }
+        if (ctx->region_renders++ == 0) {
+            HIP_TRY(ctx, hipEventRecord(ctx->events[0].first, ctx->stream), "hipEventRecord");
+            ctx->events_used = 1;
+        }
+    } else if (ctx->profiling && mode == wcpt::kModeRender) {
         if (ctx->events_used == ctx->events.size()) {
             hipEvent_t b, c;
             HIP_TRY(ctx, hipEventCreateWithFlags(&b, WCPT_PROFILE_EVENT_FLAGS), "hipEventCreate");
@@ -862,6 +876,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         return WCPT_SUCCESS;
     case WCPT_OPTION_DIAGNOSTICS:
         ctx->diagnostics = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_PROFILE_REGION:
+        if (ctx->profiling) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "profile region: set outside profiling");
+        ctx->profile_region = value ? 1 : 0;
         return WCPT_SUCCESS;
     case WCPT_OPTION_STACK:
         if (value < 0 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "stack kind %d", value);
@@ -1202,6 +1220,7 @@ int wcpt_profile_begin(wcpt_context* ctx)
     if (rc) return rc;
     ctx->profiling = true;
     ctx->events_used = 0;
+    ctx->region_renders = 0;
     return WCPT_SUCCESS;
 }
 
@@ -1209,6 +1228,8 @@ int wcpt_profile_end(wcpt_context* ctx, double* kernel_ms_total, uint32_t* launc
 {
     int rc = bind(ctx);
     if (rc) return rc;
+    const bool region = ctx->profile_region && ctx->region_renders > 0;
+    if (region) HIP_TRY(ctx, hipEventRecord(ctx->events[0].second, ctx->stream), "hipEventRecord");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     double total = 0.0;
     for (size_t i = 0; i < ctx->events_used; i++) {
@@ -1217,9 +1238,10 @@ int wcpt_profile_end(wcpt_context* ctx, double* kernel_ms_total, uint32_t* launc
         total += ms;
     }
     if (kernel_ms_total) *kernel_ms_total = total;
-    if (launches) *launches = (uint32_t)ctx->events_used;
+    if (launches) *launches = region ? ctx->region_renders : (uint32_t)ctx->events_used;
     ctx->profiling = false;
     ctx->events_used = 0;
+    ctx->region_renders = 0;
     return WCPT_SUCCESS;
 }
 
