@@ -364,6 +364,8 @@ def parse_args(argv=None):
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", type=int, default=-1,
                     help="0 megakernel, 2 wavefront, -1 per-config default (DEFAULT_KERNEL)")
+    ap.add_argument("--wf-refill", type=int, default=0,
+                    help="WCPT_OPTION_WF_REFILL: idle lanes before a trace wave refetches (0: the library default)")
     ap.add_argument("--wf-pipes", type=int, default=0,
                     help="wavefront kernel: concurrent pipelines (WCPT_OPTION_WF_PIPES; 0 = the library default)")
     ap.add_argument("--camera", default="still", choices=["still", "orbit"],
@@ -518,6 +520,8 @@ class GroupBench:
             c.set_kernel(args.kernel)
             if args.wf_pipes:
                 c.set_option(T.OPTION_WF_PIPES, args.wf_pipes)
+            if args.wf_refill:
+                c.set_option(T.OPTION_WF_REFILL, args.wf_refill)
             self.devs.append(wcpt.DeviceScene(c, scene))
         self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
         if getattr(args, "group_threads", None) is not None:
@@ -632,6 +636,8 @@ class TorchBench:
         self.ctx.set_kernel(args.kernel)
         if args.wf_pipes:
             self.ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
+        if args.wf_refill:
+            self.ctx.set_option(wcpt._lib.OPTION_WF_REFILL, args.wf_refill)
         self.dev = wcpt.DeviceScene(self.ctx, scene)
         self.ctx.create_screen(W, H)
         y0, rows = row_block(H, self.world, self.rank)

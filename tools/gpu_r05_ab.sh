@@ -33,4 +33,11 @@ for r in $(seq 1 ${EVENT_ROUNDS:-0}); do
     run events_c2_${ev}_$r 300 python3 -u bench.py --config ${EVENT_CONFIG:-c2} --no-cpu-baseline --steps 200 $A
   done
 done
+for r in $(seq 1 ${REFILL_ROUNDS:-0}); do
+  for cfg in ${REFILL_CONFIGS:-c3}; do
+    for f in ${REFILLS:-8 12 16}; do
+      run refill_${cfg}_${f}_$r 300 python3 -u bench.py --config $cfg --no-cpu-baseline --steps ${REFILL_STEPS:-30} --wf-refill $f
+    done
+  done
+done
 echo SESSION_DONE

@@ -989,8 +989,10 @@ struct PrivateStack {
 #ifndef WCPT_STACK_UNIFORM_FAST
 #define WCPT_STACK_UNIFORM_FAST 0
 #endif
+/* Spill wait in the pop's spill branch (LdsStack::pop): measured c4 -1.2 % alone, c3 -1.4 % alone, and with the
+ * deferred hit stores (pt_wavefront.hip WCPT_WF_DEFER_HIT) c3 -2.9 % / c4 -2.8 % (profiles/r05_store_wait_ab.log). */
 #ifndef WCPT_STACK_SPILL_WAIT
-#define WCPT_STACK_SPILL_WAIT 0
+#define WCPT_STACK_SPILL_WAIT 1
 #endif
 /* Entries are packed (node index | t0 bits << 32). The two storage classes are typed by address space so that
  * the compiler emits ds_read/ds_write for the LDS part and scratch_* for the spill instead of merging the two

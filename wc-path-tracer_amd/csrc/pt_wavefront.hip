@@ -183,9 +183,12 @@ constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 
 enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3, kModeIdle = 4, kModeIdlePend = 5 };
 /* Deferred hit stores: a lane whose ray is done keeps its (t, primitive) record in registers (kModeIdlePend, an idle
  * lane) and the wave writes the records when it next refills, or at its exit. On gfx9 a store counts in vmcnt, and the
- * loop's in-order vmcnt waits (the pop's, the node fetch's) would otherwise wait for it on the next iteration. */
+ * loop's in-order vmcnt waits (the pop's, the node fetch's) would otherwise wait for it on the next iteration.
+ * Measured with the in-branch spill wait (pt_device.h WCPT_STACK_SPILL_WAIT), 2 alternating rounds
+ * (profiles/r05_store_wait_ab.log): c3 4.708-4.714 against 4.848-4.856 ms (-2.9 %), c4 199.5 against 205.3 ms
+ * (-2.8 %); alone c3 -2.0 %, c4 -2.7 %. */
 #ifndef WCPT_WF_DEFER_HIT
-#define WCPT_WF_DEFER_HIT 0
+#define WCPT_WF_DEFER_HIT 1
 #endif
 
 #ifndef WCPT_WF_TRACE_SHARE
