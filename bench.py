@@ -366,6 +366,8 @@ def parse_args(argv=None):
                     help="0 megakernel, 2 wavefront, -1 per-config default (DEFAULT_KERNEL)")
     ap.add_argument("--wf-refill", type=int, default=0,
                     help="WCPT_OPTION_WF_REFILL: idle lanes before a trace wave refetches (0: the library default)")
+    ap.add_argument("--wf-fetch", type=int, default=-1, choices=[-1, 0, 1],
+                    help="WCPT_OPTION_WF_FETCH: wavefront trace fetch rounds per iteration (-1: the library's choice)")
     ap.add_argument("--wf-pipes", type=int, default=0,
                     help="wavefront kernel: concurrent pipelines (WCPT_OPTION_WF_PIPES; 0 = the library default)")
     ap.add_argument("--camera", default="still", choices=["still", "orbit"],
@@ -522,6 +524,8 @@ class GroupBench:
                 c.set_option(T.OPTION_WF_PIPES, args.wf_pipes)
             if args.wf_refill:
                 c.set_option(T.OPTION_WF_REFILL, args.wf_refill)
+            if args.wf_fetch >= 0:
+                c.set_option(T.OPTION_WF_FETCH, args.wf_fetch)
             self.devs.append(wcpt.DeviceScene(c, scene))
         self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
         if getattr(args, "group_threads", None) is not None:
@@ -638,6 +642,8 @@ class TorchBench:
             self.ctx.set_option(wcpt._lib.OPTION_WF_PIPES, args.wf_pipes)
         if args.wf_refill:
             self.ctx.set_option(wcpt._lib.OPTION_WF_REFILL, args.wf_refill)
+        if args.wf_fetch >= 0:
+            self.ctx.set_option(wcpt._lib.OPTION_WF_FETCH, args.wf_fetch)
         self.dev = wcpt.DeviceScene(self.ctx, scene)
         self.ctx.create_screen(W, H)
         y0, rows = row_block(H, self.world, self.rank)

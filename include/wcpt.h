@@ -112,6 +112,12 @@ extern "C" {
  * record is a packet on the stream: per-render pairs cost ~1.3 % of a 0.36-ms frame (c2: 0.3651-0.3660 against
  * 0.3607-0.3611 ms per frame without, profiles/r05_events_ab.log). Set it outside a profiled region. */
 #define WCPT_OPTION_PROFILE_REGION 11
+/* Wavefront trace: fetch rounds per traversal iteration. 1: the child pair of an interior lane and the triangle of a
+ * leaf lane are fetched together (a lane that descends into a leaf tests it the next iteration); 0: the leaf fetch
+ * follows the interior step, so a descent tests its first triangle in the same iteration; -1 (default): one round
+ * when a pipeline's queue holds at most 8 rays per resident trace lane (fetch latency exposed), two otherwise
+ * (issue-bound). Same results. */
+#define WCPT_OPTION_WF_FETCH 12
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

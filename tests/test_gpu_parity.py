@@ -857,6 +857,50 @@ def test_wavefront_pipelines_full_frame(gpu_ctx):
         assert ck == c1
 
 
+@pytest.mark.parametrize("fetch", [0, 1])
+@pytest.mark.parametrize("name,W,H,bounces,spp,frame,rows", [
+    ("atrium", 96, 54, 4, 1, 2, None),
+    ("cornell", 67, 45, 4, 3, 0, None),
+    ("default_dielectric", 48, 40, 3, 2, 7, None),
+    ("atrium", 200, 120, 4, 2, 1, 40),      # a row block, two samples
+])
+def test_wavefront_fetch_rounds_match_oracle(gpu_ctx, fetch, name, W, H, bounces, spp, frame, rows):
+    """WCPT_OPTION_WF_FETCH = 0 / 1: the fast-layout trace with two fetch rounds per iteration (a leaf descent tested in
+    the same iteration) and with one (interior and leaf fetches together, the descent tested next iteration) renders
+    exactly the oracle's image; auto picks one of them by queue length (small frames: one round)."""
+    s = get_scene(name)
+    init = np.random.default_rng(11).uniform(0, 1, (rows or H, W, 4)).astype(np.float32)
+    y0 = (H - rows) // 2 if rows else 0
+    gpu_ctx.set_option(wcpt._lib.OPTION_WF_FETCH, fetch)
+    try:
+        img, _ = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=spp, frame=frame, y0=y0, rows=rows, init=init,
+                            kernel=wcpt.KERNEL_WAVEFRONT)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_FETCH, -1)
+    ref, _ = oracle.render_scene(s, W, H, max_bounce=bounces, samples=spp, frame=frame, y0=y0, rows=rows,
+                                 image=init, threads=8)
+    assert_close(img, ref)
+
+
+def test_wavefront_fetch_rounds_full_frame(gpu_ctx):
+    """1080p atrium frame, 2 samples: one and two fetch rounds per trace iteration give the bit-identical frame, and a
+    bad option value is refused."""
+    s = get_scene("atrium")
+    W, H = 1920, 1080
+    init = np.zeros((H, W, 4), np.float32)
+    out = []
+    for fetch in (0, 1):
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_FETCH, fetch)
+        try:
+            out.append(gpu_render(gpu_ctx, s, W, H, bounces=4, spp=2, frame=3, init=init,
+                                  kernel=wcpt.KERNEL_WAVEFRONT)[0])
+        finally:
+            gpu_ctx.set_option(wcpt._lib.OPTION_WF_FETCH, -1)
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    with pytest.raises(wcpt.WcptError):
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_FETCH, 2)
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("channels", [3, 4, 8])
 def test_gather_output_equals_image(gpu_ctx, kernel, channels):

@@ -40,4 +40,14 @@ for r in $(seq 1 ${REFILL_ROUNDS:-0}); do
     done
   done
 done
+for r in $(seq 1 ${FETCH_ROUNDS:-0}); do
+  for f in 0 1; do
+    for cfg in ${FETCH_CONFIGS:-c3 c4}; do
+      run fetch_${cfg}_${f}_$r 300 python3 -u bench.py --config $cfg --no-cpu-baseline --steps ${FETCH_STEPS:-30} --wf-fetch $f ${FETCH_ARGS:-}
+    done
+    for cfg in ${FETCH_BLOCKS:-}; do
+      run fetchblock_${cfg}_${f}_$r 300 python3 -u tools/block_balance.py --config $cfg --ns 8 --skip-full --wf-fetch $f
+    done
+  done
+done
 echo SESSION_DONE

@@ -28,6 +28,7 @@ struct LaunchArgs {
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
+    int wf_fetch;                /* wavefront trace fetch rounds per iteration: -1 auto, 0 two, 1 one (WCPT_OPTION_WF_FETCH) */
     bool wf_fast;                /* wavefront trace: draw 0 has packed stack refs, 24-bit record offsets, leaves of < 255
                                     index positions on derived records (kTriFlagSmallLeaves, kTriFlagLeafRecords) and a known
                                     node count (table flags 1|2|4|8, word 2 high half > 0) */

@@ -264,9 +264,10 @@ __device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, const
 
 /* GEO: 0 any draws; 1 one draw command (the reference's case, kernel-uniform geometry in scalar registers); 2 one draw
  * whose table flags allow packed stack refs, 24-bit record offsets and buffer-resource node loads (the host checks
- * them), so the loop carries no branches for the other layouts. */
+ * them), so the loop carries no branches for the other layouts; 3 the same with one fetch round per iteration
+ * (wf_fetch_once). */
 template <bool COUNT, bool DIAG, int GEO, int LDSN>
-__global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
+__global__ __launch_bounds__(64, GEO >= 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
                                                   const wcpt_draw_command* __restrict__ draws,
                                                   const uint64_t* __restrict__ tri_records, WfBuffers b,
                                                   uint32_t* __restrict__ status, unsigned long long* __restrict__ counters,
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
     Geom g0 = {}, gl = g0;
     constexpr bool SINGLE = GEO >= 1;
     if (SINGLE) g0 = load_geom(draws, tri_records, 0); /* kernel-uniform: scalar registers */
-    if (GEO == 2) {
+    if (GEO >= 2) {
         g0.packed = true;
         g0.idx24 = true;
     }
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                     stk.pop(ni, t0);
                     ref_pop<COUNT>(rf);
                     if (!(t0 > rt)) {
-                        const uint2 lc = (GEO == 2 && WCPT_WF_SMALL_LEAVES) ? node_ref_lc_small(ni)
+                        const uint2 lc = (GEO >= 2 && WCPT_WF_SMALL_LEAVES) ? node_ref_lc_small(ni)
                                                                             : node_ref_lc(g.packed, g.bvh, ni);
                         cursor_from(lc.x, lc.y, g, ca, cb, cr, mode);
                     }
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 const float farT0 = leftFirst ? r0 : l0;
                 if (passFar && (COUNT || !WCPT_WF_PUSH_CULL || !(farT0 > rt))) {
                     const NodeV& F = leftFirst ? R : L;
-                    const uint32_t fref = (GEO == 2 && WCPT_WF_SMALL_LEAVES) ? node_ref_small(F.b.z, F.b.w)
+                    const uint32_t fref = (GEO >= 2 && WCPT_WF_SMALL_LEAVES) ? node_ref_small(F.b.z, F.b.w)
                                                                             : node_ref(g.packed, leftFirst ? ca + 1 : ca, F.b.z, F.b.w);
                     if (!stk.push(fref, farT0))
                         overflow = true;
@@ -503,9 +504,23 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 return tri_from_indices(g.indices, g.vertices, ca, draw_vertex_count(tri_records, SINGLE ? 0u : d));
             };
             diag_mark<DIAG>(tim, tprev, 3); /* pop */
+            if (GEO == 3 && WCPT_WF_PAIR_RSRC && WCPT_WF_LEAF_RECORDS) {
+                /* one fetch round per iteration (GEO 3, wf_fetch_once): the child pair of an interior lane and the
+                 * triangle of a leaf lane are both issued before either is waited for; a lane that descends into a leaf
+                 * tests it next iteration */
+                const bool fi = mode == kModeInterior, fl = mode == kModeLeaf;
+                NodeV L, R;
+                TriE tr;
+                if (fi) load_pair_rsrc(g.rsrc, ca, L, R);
+                if (fl) tr = load_tri_rsrc(g.trsrc, ca * 16u);
+                if (fi) interior_step(L, R);
+                diag_mark<DIAG>(tim, tprev, 2);
+                if (fl) leaf_step(tr);
+                diag_mark<DIAG>(tim, tprev, 1);
+            } else {
             if (mode == kModeInterior) {
                 NodeV L, R;
-                if (WCPT_WF_PAIR_RSRC && (GEO == 2 || g.nodes)) {
+                if (WCPT_WF_PAIR_RSRC && (GEO >= 2 || g.nodes)) {
                     load_pair_rsrc(g.rsrc, ca, L, R);
                 } else {
                     L = load_node(g.bvh, ca);
@@ -517,7 +532,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             if (mode == kModeLeaf) {
                 /* one triangle per step, from the single records (pair records measured slower here: most
                  * atrium leaves hold 1-2 triangles, and the wider record costs fetch bytes and VGPRs) */
-                if (GEO == 2 && WCPT_WF_LEAF_RECORDS) {
+                if (GEO >= 2 && WCPT_WF_LEAF_RECORDS) {
                     /* every leaf triangle has its record (kTriFlagLeafRecords); the load goes through a buffer resource
                      * bounded by the draw's records, so a BVH rewritten behind the runtime's cache (wcpt.h
                      * WCPT_OPTION_TRIANGLE_CACHE) reads zeros -- a triangle no ray accepts -- instead of past them */
@@ -528,6 +543,7 @@ __global__ __launch_bounds__(64, GEO == 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 }
             }
             diag_mark<DIAG>(tim, tprev, 1);
+            }
             if (mode == kModeDone) {
                 /* Intersect result; wf_shade rebuilds the winner's normal and material (:204-208) */
                 if (WCPT_WF_DEFER_HIT) {
@@ -872,6 +888,7 @@ static hipError_t wf_dispatch(int mode, int geo, int ldsn, bool query, int& bpc,
                                          : wf_variant<true, true, 0, 10>(query, bpc, a, b, tg, sg, st);
     if (!single) return wf_variant<false, false, 0, 10>(query, bpc, a, b, tg, sg, st);
     if (geo == 2) return wf_variant<false, false, 2, 10>(query, bpc, a, b, tg, sg, st);
+    if (geo == 3) return wf_variant<false, false, 3, 10>(query, bpc, a, b, tg, sg, st);
     if (ldsn == 16) return wf_variant<false, false, 1, 16>(query, bpc, a, b, tg, sg, st);
     if (ldsn == 24) return wf_variant<false, false, 1, 24>(query, bpc, a, b, tg, sg, st);
     return wf_variant<false, false, 1, 10>(query, bpc, a, b, tg, sg, st);
@@ -883,6 +900,23 @@ static int wf_geo(const LaunchArgs& a, int mode, int ldsn)
 {
     if (a.sd.drawCommandCount != 1) return 0;
     return (WCPT_WF_GEO_FAST && a.wf_fast && mode == kModeRender && ldsn == 10) ? 2 : 1;
+}
+
+/* One fetch round per trace iteration (GEO 3) or two (GEO 2: a lane that descends into a leaf tests its first
+ * triangle in the same iteration, after the interior lanes' fetch). One round overlaps the interior and leaf lanes'
+ * fetches, which pays where fetch latency is exposed -- few queued rays per resident lane, so much of the launch is
+ * its tail -- and costs an iteration per leaf descent, which loses where the chip is issue-bound on a long queue.
+ * Measured (profiles/r05_fetch_once_ab.log): c3 (4.0 rays per lane per pipeline) 4.52 against 4.66 ms; c4 (15.8)
+ * 203.6 against 199.6 ms. WCPT_OPTION_WF_FETCH: -1 (default) by that ratio, 0 two rounds, 1 one round. */
+#ifndef WCPT_WF_FETCH_ONCE_RATIO
+#define WCPT_WF_FETCH_ONCE_RATIO 8
+#endif
+static int wf_trace_geo(const LaunchArgs& a, int mode, int ldsn, uint32_t P, uint32_t trace_grid)
+{
+    const int geo = wf_geo(a, mode, ldsn);
+    if (geo != 2 || a.wf_fetch == 0) return geo;
+    if (a.wf_fetch > 0) return 3;
+    return (uint64_t)P <= (uint64_t)WCPT_WF_FETCH_ONCE_RATIO * 64ull * trace_grid ? 3 : 2;
 }
 
 static hipError_t sort_queue(const LaunchArgs& a, WfState& s, const WfBuffers& b, uint32_t P, int cus,
@@ -950,7 +984,8 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
     const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
     if (pipe >= tiles) return hipSuccess;
     const uint32_t P = min(((tiles - pipe + npipes - 1u) / npipes) * 64u, a.W * a.rows); /* as pipe_begin */
-    const int geo = wf_geo(a, mode, ldsn); /* one draw: the reference's case (PathTracingRenderer.jai:251) */
+    /* one draw: the reference's case (PathTracingRenderer.jai:251) */
+    const int geo = wf_trace_geo(a, mode, ldsn, P, trace_grid);
     hipError_t e = hipSuccess;
     /* each iteration advances every live path by one traced segment; a path needs <= samples*(maxBounce+1), or
      * with the primary records reused (wf_shade) maxBounce+1 for sample 0 and maxBounce for each later sample */
@@ -987,7 +1022,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     hipError_t e = cu_count(s0, cus);
     if (e != hipSuccess) return e;
     const int ldsn = (lds_stack == 16 || lds_stack == 24) ? lds_stack : 10;
-    const int geo = wf_geo(a, mode, ldsn);
+    const int geo = wf_geo(a, mode, ldsn); /* GEO 3 (wf_trace_geo) runs at GEO 2's occupancy: both 8 waves/SIMD */
     int& bpc = s0.trace_bpc[mode][geo][ldsn == 10 ? 0 : (ldsn == 16 ? 1 : 2)];
     if (bpc == 0) {
         e = wf_dispatch(mode, geo, ldsn, true, bpc, a, WfBuffers{}, 0, 0, stream);

@@ -152,6 +152,7 @@ struct wcpt_context {
     int wf_stack = 10;                 /* WCPT_OPTION_WF_STACK: LDS stack entries of the wavefront trace kernel */
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
+    int wf_fetch = -1;                 /* WCPT_OPTION_WF_FETCH */
     int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (round 2 with the any-hit last segment, c3: 4 / 8 / 12 / 16 / 20 -> 5.80 / 5.74 / 5.71 / 5.75 / 5.80 ms) */
 #ifndef WCPT_WF_PIPES_DEFAULT
 #define WCPT_WF_PIPES_DEFAULT 2
@@ -550,6 +551,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.pair_records = false;
     a.wf_fast = false;
     a.wf_refill = (uint32_t)ctx->wf_refill;
+    a.wf_fetch = ctx->wf_fetch;
     a.mk_tile_order = (uint32_t)ctx->mk_tile_order;
     hipEvent_t e0 = nullptr, e1 = nullptr;
 /* Profiling events time the launches only: no system-scope fence when they are recorded (hip_runtime_api.h,
@@ -876,6 +878,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         return WCPT_SUCCESS;
     case WCPT_OPTION_DIAGNOSTICS:
         ctx->diagnostics = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_WF_FETCH:
+        if (value < -1 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wavefront fetch rounds %d", value);
+        ctx->wf_fetch = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PROFILE_REGION:
         if (ctx->profiling) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "profile region: set outside profiling");

@@ -53,6 +53,7 @@ DEFAULT_WF_REFILL = 12  # wcpt_runtime.hip
 OPTION_MK_TILE_ORDER = 9
 OPTION_WF_PIPES = 10
 OPTION_PROFILE_REGION = 11
+OPTION_WF_FETCH = 12
 DEFAULT_WF_PIPES = 2  # wcpt_runtime.hip
 
 # gather payload formats (wcpt_set_gather_output, wcpt_group_set_output)
