@@ -91,9 +91,9 @@ extern "C" {
 /* Traversal stack entries carry the deferred child's (left, count) (1, default, when the draw's BVH buffer is a
  * context buffer of < 2^24 nodes) so a pop needs no node fetch; 0: entries hold node indices. Same results. */
 #define WCPT_OPTION_PACKED_REFS 7
-/* Wavefront trace: a wave fetches new rays once this many of its 64 lanes are idle (1..64, default 12: fewer,
- * fuller fetch rounds; c3 9.0 -> 8.2 ms at 12 against 1; with the any-hit last segment 5.71 ms at 12 against 5.80 at
- * 20). */
+/* Wavefront trace: a wave fetches new rays once this many of its 64 lanes are idle (1..64, default 20: fewer,
+ * fuller fetch rounds; c3 9.0 -> 8.2 ms at 12 against 1; round 5, with the finished lanes' hit records stored at the
+ * refill: c4 197.8-198.2 ms at 20 against 199.5 at 12 and 201.3 at 32, c3 unchanged within the spread). */
 #define WCPT_OPTION_WF_REFILL 8
 /* Megakernel tile order: 0 each XCD walks a contiguous band of 8x8 tiles; 1 scattered (tile b * m mod tiles), so the
  * tiles resident on a CU at once come from all over the frame; 3, 4, 5, 6 XCD bands striped by 1, 2, 4, 8 tile rows

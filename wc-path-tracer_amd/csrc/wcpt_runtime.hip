@@ -153,7 +153,7 @@ struct wcpt_context {
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_fetch = -1;                 /* WCPT_OPTION_WF_FETCH */
-    int wf_refill = 12;                /* WCPT_OPTION_WF_REFILL (round 2 with the any-hit last segment, c3: 4 / 8 / 12 / 16 / 20 -> 5.80 / 5.74 / 5.71 / 5.75 / 5.80 ms) */
+    int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (round 5 with the deferred hit stores, c4: 8 / 12 / 16 / 20 / 24 / 32 -> 203.5 / 199.6 / 198.9 / 198.0 / 198.6 / 201.4 ms; c3 flat; profiles/r05_fetch_once_ab.log) */
 #ifndef WCPT_WF_PIPES_DEFAULT
 #define WCPT_WF_PIPES_DEFAULT 2
 #endif

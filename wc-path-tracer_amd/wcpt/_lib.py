@@ -49,7 +49,7 @@ OPTION_TRIANGLE_CACHE = 5
 OPTION_PAIR_RECORDS = 6
 OPTION_PACKED_REFS = 7
 OPTION_WF_REFILL = 8
-DEFAULT_WF_REFILL = 12  # wcpt_runtime.hip
+DEFAULT_WF_REFILL = 20  # wcpt_runtime.hip
 OPTION_MK_TILE_ORDER = 9
 OPTION_WF_PIPES = 10
 OPTION_PROFILE_REGION = 11
