@@ -1071,28 +1071,12 @@ __device__ __forceinline__ f3 triangle_normal(uint32_t prim, uint32_t draw, cons
     return normalize(cross(e.e1, e.e2));
 }
 
-/* The single-record word of triangle_normal's fast case, loaded on its own (wf_shade issues it before its next
- * slot's stream loads): false when the triangle takes the index path. */
-__device__ __forceinline__ bool tri_record_normal_load(uint32_t prim, uint32_t draw,
-                                                       const uint64_t* __restrict__ tri_records, v4f& r2)
-{
-    const uint32_t k = prim / 3u;
-    if (tri_records && k * 3u == prim && k < (uint32_t)tri_records[kTriTableWords * draw + 2u]) {
-        const gtri_ptr t = (gtri_ptr)(uintptr_t)tri_records[kTriTableWords * draw];
-        r2 = t[3ull * k + 2u];
-        return true;
-    }
-    return false;
-}
-
 /* Intersect epilogue (:204-208) for winner `prim` (kNoPrim, kSpherePrim | sphere, or the index position of
- * a triangle of draw `draw`) at distance t. pre_ok: the triangle's record word was loaded already (pre_r2,
- * tri_record_normal_load). */
+ * a triangle of draw `draw`) at distance t. */
 __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t prim, uint32_t draw,
                                            const wcpt_sphere* __restrict__ spheres,
                                            const wcpt_draw_command* __restrict__ draws,
-                                           const uint64_t* __restrict__ tri_records, bool pre_ok = false,
-                                           v4f pre_r2 = v4f{})
+                                           const uint64_t* __restrict__ tri_records)
 {
     Hit h;
     h.t = t;
@@ -1107,8 +1091,6 @@ __device__ __forceinline__ Hit resolve_hit(const Ray& ray, float t, uint32_t pri
             const f3 ph = ray.origin + t * ray.direction;
             h.normal = (ph - c) / s.radius;                        /* :145 */
             h.material = s.material;
-        } else if (pre_ok) {
-            h.normal = mk3(pre_r2.y, pre_r2.z, pre_r2.w); /* :173 (the record's n), material 0 (:175) */
         } else {
             h.normal = triangle_normal(prim, draw, draws, tri_records); /* :173, material 0 (:175) */
         }
