@@ -39,10 +39,7 @@ namespace dev {
 #define WCPT_TRACE_CHUNK 64
 #endif
 constexpr uint32_t kTraceChunk = WCPT_TRACE_CHUNK;
-#ifndef WCPT_SHADE_BLOCK
-#define WCPT_SHADE_BLOCK 256
-#endif
-constexpr int kShadeBlock = WCPT_SHADE_BLOCK;
+constexpr int kShadeBlock = 256;
 
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -575,9 +572,6 @@ __global__ __launch_bounds__(64, GEO >= 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
 #ifndef WCPT_SHADE_PREFETCH
 #define WCPT_SHADE_PREFETCH 0 /* measured +0.8 % on c3, +0.7 % on c4: off */
 #endif
-#ifndef WCPT_SHADE_PIPE
-#define WCPT_SHADE_PIPE 0 /* the prefetch with the winner's record issued before the next slot's loads */
-#endif
 /* One input queue slot of wf_shade: pixel, ray, light, transmittance and the trace's Intersect record. */
 struct PathIn {
     uint32_t pix;
@@ -609,7 +603,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
     const uint32_t n = *b.count_in;
     Counters cnt = {};
     const uint32_t stride = gridDim.x * blockDim.x;
-#if WCPT_SHADE_PREFETCH || WCPT_SHADE_PIPE
+#if WCPT_SHADE_PREFETCH
     /* The path state of the thread's next queue slot is loaded before the current one is shaded: the streams (path
      * state in queue order, coalesced) have one iteration of the grid-stride loop to arrive instead of stalling its
      * start, and the dependent gathers of the current path (normal, material) overlap them. */
@@ -621,21 +615,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
         uint32_t p = 0, sample = 0, seed = 0, prim0 = kNoPrim;
         float rt0 = kInfinity;
         PathState ps;
-#if WCPT_SHADE_PIPE
-        const PathIn cur = nxt;
-        /* the winner's record word first, then the next slot's stream loads: vmcnt retires in issue order, so the
-         * gather the shading waits for is older than the loads it does not wait for (the barriers keep that order) */
-        const uint32_t hprim = __float_as_uint(cur.hi.y);
-        v4f pre_r2 = {};
-        bool pre_ok = false;
-        if (w < n && hprim != kNoPrim && !(hprim & kSpherePrim)) {
-            if (sd.drawCommandCount == 1u) pre_ok = tri_record_normal_load(hprim, 0u, tri_records, pre_r2);
-            else pre_ok = tri_record_normal_load(hprim, __float_as_uint(cur.hi.z), tri_records, pre_r2);
-        }
-        asm volatile("" ::: "memory");
-        nxt = load_path_in(b, w + stride, n);
-        asm volatile("" ::: "memory");
-#elif WCPT_SHADE_PREFETCH
+#if WCPT_SHADE_PREFETCH
         const PathIn cur = nxt;
         nxt = load_path_in(b, w + stride, n);
 #else
@@ -661,15 +641,9 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
             float4 h4 = hi;
             f3 result = mk3(0.0f, 0.0f, 0.0f);
             bool summed = false; /* result holds b.result[p] + this call's finished samples */
-#if !WCPT_SHADE_PIPE
-            const bool pre_ok = false;
-            const v4f pre_r2 = {};
-#endif
-            bool first = true;
             for (;;) {
                 const Hit h = resolve_hit(ps.ray, h4.x, __float_as_uint(h4.y), __float_as_uint(h4.z), spheres, draws,
-                                          tri_records, first && pre_ok, pre_r2);
-                first = false;
+                                          tri_records);
                 if (COUNT && h.hit) cnt.hits++;
                 f3 L;
                 if (!path_shade(ps, h, seed, sd, mats, L, sample + 1u == sd.samples)) {
