@@ -50,4 +50,11 @@ for r in $(seq 1 ${FETCH_ROUNDS:-0}); do
     done
   done
 done
+for r in $(seq 1 ${PIPEB_ROUNDS:-0}); do
+  for pp in ${PIPEBS:-2 3}; do
+    for cfg in ${PIPEB_CONFIGS:-c3 c4}; do
+      run pipes_${cfg}_${pp}_$r 300 python3 -u bench.py --config $cfg --no-cpu-baseline --steps ${PIPEB_STEPS:-30} --wf-pipes $pp
+    done
+  done
+done
 echo SESSION_DONE
