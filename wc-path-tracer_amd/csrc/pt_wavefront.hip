@@ -1042,7 +1042,11 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     const uint32_t shade_grid = WCPT_SHADE_BLOCKS_PER_CU > 0 ? (uint32_t)(cus * WCPT_SHADE_BLOCKS_PER_CU)
                                                              : (P + dev::kShadeBlock - 1) / dev::kShadeBlock;
     sort_rays = sort_rays && a.sd.drawCommandCount > 0;
-    uint32_t K = (uint32_t)(pipes < 1 ? 1 : (pipes > kWfMaxPipes ? kWfMaxPipes : pipes));
+    /* pipelines: the option's count, or (0, the default) 3 when the frame holds at most 8 paths per resident trace lane
+     * -- the launches are short and their tails weigh, so a third chain overlaps them (c3 4.41-4.46 against 4.50-4.55
+     * ms with two) -- and 2 on longer queues (c4 199.5 against 197.9 ms with two; profiles/r05_pipes_ab.log) */
+    uint32_t K = (uint32_t)(pipes > kWfMaxPipes ? kWfMaxPipes : pipes);
+    if (pipes < 1) K = (uint64_t)a.W * a.rows <= (uint64_t)WCPT_WF_FETCH_ONCE_RATIO * 64ull * trace_grid ? 3u : 2u;
     if (sort_rays || mode == kModeDiag) K = 1; /* one sort scratch and one diagnostics block */
     const uint32_t tiles = tilesX * tilesY;
     if (K > tiles) K = tiles;

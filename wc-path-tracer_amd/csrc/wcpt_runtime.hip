@@ -155,9 +155,9 @@ struct wcpt_context {
     int wf_fetch = -1;                 /* WCPT_OPTION_WF_FETCH */
     int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (round 5 with the deferred hit stores, c4: 8 / 12 / 16 / 20 / 24 / 32 -> 203.5 / 199.6 / 198.9 / 198.0 / 198.6 / 201.4 ms; c3 flat; profiles/r05_fetch_once_ab.log) */
 #ifndef WCPT_WF_PIPES_DEFAULT
-#define WCPT_WF_PIPES_DEFAULT 2
+#define WCPT_WF_PIPES_DEFAULT 0
 #endif
-    int wf_pipes = WCPT_WF_PIPES_DEFAULT; /* WCPT_OPTION_WF_PIPES (2: c3 -2%, a c4 8-way row block -10%) */
+    int wf_pipes = WCPT_WF_PIPES_DEFAULT; /* WCPT_OPTION_WF_PIPES (0 = by queue length, pt_wavefront.hip launch_wavefront) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload / free and every option change */
@@ -854,7 +854,7 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         ctx->wf_refill = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_WF_PIPES:
-        if (value < 1 || value > wcpt::kWfMaxPipes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pipelines %d", value);
+        if (value < 0 || value > wcpt::kWfMaxPipes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pipelines %d", value);
         ctx->wf_pipes = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_MK_TILE_ORDER:

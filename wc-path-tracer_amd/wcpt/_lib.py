@@ -54,7 +54,7 @@ OPTION_MK_TILE_ORDER = 9
 OPTION_WF_PIPES = 10
 OPTION_PROFILE_REGION = 11
 OPTION_WF_FETCH = 12
-DEFAULT_WF_PIPES = 2  # wcpt_runtime.hip
+DEFAULT_WF_PIPES = 0  # wcpt_runtime.hip: by queue length (2 or 3)
 
 # gather payload formats (wcpt_set_gather_output, wcpt_group_set_output)
 PAYLOAD_RGB32F = 3
