@@ -16,7 +16,8 @@ S=$OUT/summaries; mkdir -p "$S"
 cp "$OUT/sq/build_id" "$S/build_id"
 python3 tools/profile_summaries.py "$OUT/sq" --configs $CFGS --out "$S" --source "round 5 final build ($TAG)" || exit 1
 for c in c3 c4; do
-  case " $CFGS " in *" $c "*) python3 tools/traffic_split.py "$OUT/sq/sq_$c" --json "$S/traffic_split_$c.json" > "$S/traffic_split_$c.log" || exit 1;; esac
+  PF=2; [ $c = c3 ] && PF=3  # wavefront pipelines per frame (tools/profile_summaries.py PIPES)
+  case " $CFGS " in *" $c "*) python3 tools/traffic_split.py "$OUT/sq/sq_$c" --per-frame $PF --json "$S/traffic_split_$c.json" > "$S/traffic_split_$c.log" || exit 1;; esac
 done
 for c in $CFGS; do
   f=$(find "$OUT/sq/prof_$c" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" "$S/${c}_kernel_stats.csv"

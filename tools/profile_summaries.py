@@ -32,6 +32,9 @@ SPEC = {
            "control between them", "wf_trace<false,wf_shade<false,wf_init<false"),
 }
 MIX = ("ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "INT32", "INT64", "CVT")
+# wavefront pipelines per frame (one wf_init each: the per-frame divisor of the PMC passes). The library picks them by
+# queue length (WCPT_OPTION_WF_PIPES 0): 3 for the 1080p atrium (2.1 M paths, 4 per resident trace lane), 2 at 4K
+PIPES = {"c3": 3, "c4": 2}
 
 
 def kernel_ms(d, cfg, filt):
@@ -75,7 +78,8 @@ def main():
         pm = [py, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--config", base,
               "--camera", camera,
               "--kernel-id", str(kid), "--build-id", build, "--json", os.path.join(a.out, f"pmc_traffic_{cfg}.json")]
-        pm += ["--kernel", frame_filters, "--frame-kernel", "wf_init<false"] if frame_filters else ["--kernel", filt]
+        pm += (["--kernel", frame_filters, "--frame-kernel", "wf_init<false", "--per-frame", str(PIPES[base])]
+               if frame_filters else ["--kernel", filt])
         subprocess.run(pm, check=True, stdout=subprocess.DEVNULL)
         m, n = counters(a.dir, cfg, filt)
         tot = m.get("SQ_INSTS_VALU")
