@@ -39,7 +39,9 @@ extern "C" {
  * 3: groups overlap each frame's gather with the next frame's render; wcpt_group_create_ex (transports),
  *    wcpt_group_unique_id / wcpt_group_create_rank (one process per device), wcpt_group_set_option, wcpt_group_info.
  * 4: WCPT_GROUP_OPTION_THREADS (each local rank's share of a frame issued from a host thread of its own);
- *    wcpt_group_info gained issue_threads; wcpt_group_set_output reads `bytes` in every process. */
+ *    wcpt_group_info gained issue_threads; wcpt_group_set_output reads `bytes` in every process. Later additions that
+ *    keep the layouts and calls (no version step): WCPT_GROUP_TRANSPORT_DIRECT, WCPT_OPTION_PROFILE_REGION,
+ *    WCPT_OPTION_WF_FETCH, WCPT_OPTION_WF_PIPES 0 (automatic, now the default). */
 #define WCPT_ABI_VERSION 4
 
 /* ---- error codes (VkResult-compatible where a VkResult exists) ---------------------------------- */
