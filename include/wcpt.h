@@ -341,8 +341,8 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          fewer devices: every rank still has its own context, streams and payloads), or
  *                          WCPT_GROUP_TRANSPORT_DIRECT (each render writes its block into the root's frame itself).
  *                          Status: RCCL between n > 1 distinct GPUs over xGMI is UNVERIFIED on hardware here (the
- *                          development boxes have one GPU). The one-process-per-device form (below) has run with 2
- *                          ranks on one GPU over RCCL's socket transport (bench.py --rccl-rehearsal, frame verified
+ *                          development boxes have one GPU). The one-process-per-device form (below) has run with 2,
+ *                          4 and 8 ranks on one GPU over RCCL's socket transport (bench.py --rccl-rehearsal, frame verified
  *                          bit-exact); the COPY and DIRECT transports run the same bookkeeping and are tested with 2-8
  *                          ranks on one GPU.
  *   wcpt_group_unique_id / wcpt_group_create_rank   one process per device (e.g. one process per GPU under
