@@ -121,6 +121,10 @@ extern "C" {
  * when a pipeline's queue holds at most 8 rays per resident trace lane (fetch latency exposed), two otherwise
  * (issue-bound). Same results. */
 #define WCPT_OPTION_WF_FETCH 12
+/* Wavefront: the path-persistent trace, one launch per frame in which each lane runs its path's segments one after
+ * another and shades between them, for one sample per pixel on one-draw scenes. -1 (default): where every path of a
+ * pipeline has a resident lane from the start (row blocks), 0 never, 1 whenever eligible. Same results. */
+#define WCPT_OPTION_WF_PERSIST 13
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

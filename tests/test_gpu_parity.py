@@ -882,6 +882,51 @@ def test_wavefront_fetch_rounds_match_oracle(gpu_ctx, fetch, name, W, H, bounces
     assert_close(img, ref)
 
 
+@pytest.mark.parametrize("persist", [0, 1])
+@pytest.mark.parametrize("name,W,H,bounces,frame,rows", [
+    ("atrium", 96, 54, 4, 2, None),
+    ("cornell", 67, 45, 4, 0, None),
+    ("default_dielectric", 48, 40, 3, 7, None),
+    ("atrium", 200, 120, 4, 1, 40),      # a row block
+    ("reference_init", 64, 48, 3, 0, None),
+])
+def test_wavefront_persist_matches_oracle(gpu_ctx, persist, name, W, H, bounces, frame, rows):
+    """WCPT_OPTION_WF_PERSIST = 0 / 1: the per-bounce trace + shade launches and the path-persistent trace (each lane
+    runs its path's segments one after another and shades between them) render exactly the oracle's image."""
+    s = get_scene(name)
+    init = np.random.default_rng(13).uniform(0, 1, (rows or H, W, 4)).astype(np.float32)
+    y0 = (H - rows) // 2 if rows else 0
+    gpu_ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, persist)
+    try:
+        img, _ = gpu_render(gpu_ctx, s, W, H, bounces=bounces, spp=1, frame=frame, y0=y0, rows=rows, init=init,
+                            kernel=wcpt.KERNEL_WAVEFRONT)
+    finally:
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, -1)
+    ref, _ = oracle.render_scene(s, W, H, max_bounce=bounces, samples=1, frame=frame, y0=y0, rows=rows,
+                                 image=init, threads=8)
+    assert_close(img, ref)
+
+
+def test_wavefront_persist_full_frame_and_block(gpu_ctx):
+    """1080p atrium: the path-persistent trace forced on gives the bit-identical frame of the per-bounce launches, and
+    so does a 135-row block (where it is the automatic choice); a bad option value is refused."""
+    s = get_scene("atrium")
+    W, H = 1920, 1080
+    for rows, y0 in ((None, 0), (135, 540)):
+        init = np.zeros((rows or H, W, 4), np.float32)
+        out = []
+        for persist in (0, 1):
+            gpu_ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, persist)
+            try:
+                out.append(gpu_render(gpu_ctx, s, W, H, bounces=4, spp=1, frame=3, y0=y0, rows=rows, init=init,
+                                      kernel=wcpt.KERNEL_WAVEFRONT)[0])
+            finally:
+                gpu_ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, -1)
+        assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    with pytest.raises(wcpt.WcptError):
+        gpu_ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, 2)
+
+
 def test_wavefront_fetch_rounds_full_frame(gpu_ctx):
     """1080p atrium frame, 2 samples: one and two fetch rounds per trace iteration give the bit-identical frame, and a
     bad option value is refused."""

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--kernel", type=int, default=-1, help="WCPT_KERNEL_* (default: bench.py's for the config)")
     ap.add_argument("--wf-pipes", type=int, default=0, help="WCPT_OPTION_WF_PIPES (0: the library default)")
     ap.add_argument("--wf-fetch", type=int, default=-1, help="WCPT_OPTION_WF_FETCH (-1: auto)")
+    ap.add_argument("--wf-persist", type=int, default=-1, help="WCPT_OPTION_WF_PERSIST (-1: auto)")
     ap.add_argument("--skip-full", action="store_true", help="do not time the full frame (full/N columns then 0)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
@@ -41,6 +42,7 @@ def main():
     if a.wf_pipes:
         ctx.set_option(wcpt._lib.OPTION_WF_PIPES, a.wf_pipes)
     ctx.set_option(wcpt._lib.OPTION_WF_FETCH, a.wf_fetch)
+    ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, a.wf_persist)
     dev = wcpt.DeviceScene(ctx, s)
     ctx.create_screen(W, H)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]

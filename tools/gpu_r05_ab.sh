@@ -57,4 +57,11 @@ for r in $(seq 1 ${PIPEB_ROUNDS:-0}); do
     done
   done
 done
+for r in $(seq 1 ${PERSIST_ROUNDS:-0}); do
+  for f in 0 -1; do
+    for cfg in ${PERSIST_BLOCKS:-c3}; do
+      run persistblock_${cfg}_${f}_$r 300 python3 -u tools/block_balance.py --config $cfg --ns ${PERSIST_NS:-8} --skip-full --wf-persist $f
+    done
+  done
+done
 echo SESSION_DONE

@@ -29,6 +29,7 @@ struct LaunchArgs {
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
     int wf_fetch;                /* wavefront trace fetch rounds per iteration: -1 auto, 0 two, 1 one (WCPT_OPTION_WF_FETCH) */
+    int wf_persist;              /* path-persistent trace: -1 auto, 0 off, 1 wherever eligible (WCPT_OPTION_WF_PERSIST) */
     bool wf_fast;                /* wavefront trace: draw 0 has packed stack refs, 24-bit record offsets, leaves of < 255
                                     index positions on derived records (kTriFlagSmallLeaves, kTriFlagLeafRecords) and a known
                                     node count (table flags 1|2|4|8, word 2 high half > 0) */
@@ -84,6 +85,7 @@ struct WfState {
     size_t sort_temp_bytes = 0;
     int cus = 0;                   /* compute units of the context's device (0 = not yet queried)          */
     int trace_bpc[3][3][3] = {};   /* trace-kernel blocks per CU by (mode, geometry variant, LDS stack)      */
+    int persist_bpc = 0;           /* the path-persistent trace's blocks per CU                             */
 };
 
 /* Concurrent wavefront pipelines (WCPT_OPTION_WF_PIPES): pipeline j of K owns the 8x8 tiles t with t % K == j and

@@ -119,6 +119,14 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_LEAF_RECORDS
 #define WCPT_WF_LEAF_RECORDS 1 /* the fast layout also requires kTriFlagLeafRecords: leaf steps need no index path */
 #endif
+/* Path-persistent trace (PERSIST instances, wf_persist_ok): one launch runs every segment of its paths. A lane whose
+ * ray is done shades it in place (resolve_hit, path_shade, the next segment's sphere loop, or the pixel's store) and
+ * goes on with the path's next segment, so no path waits for the slowest ray of its bounce; the wave shades once
+ * `refill` of its lanes wait, or when none is tracing. Used where a pipeline's queue is short (row blocks), for one
+ * sample per pixel. */
+#ifndef WCPT_WF_PERSIST_WAVES
+#define WCPT_WF_PERSIST_WAVES 4
+#endif
 #ifndef WCPT_WF_GEO2_WAVES
 #define WCPT_WF_GEO2_WAVES 8 /* occupancy floor of the fast-layout trace (waves per SIMD) */
 #endif
@@ -180,7 +188,8 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
  * entries run within 1%, 24 is 13% slower -- the traversal is bound by node-fetch latency, not the spill). */
 constexpr int wf_lds_per_wave(int n) { return n * 512; }
 constexpr int wf_waves_per_simd(int n) { return (163840 / wf_lds_per_wave(n)) / 4 < 8 ? (163840 / wf_lds_per_wave(n)) / 4 : 8; }
-enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3, kModeIdle = 4, kModeIdlePend = 5 };
+enum : uint32_t { kModeInterior = 0, kModeLeaf = 1, kModePop = 2, kModeDone = 3, kModeShade = 4, kModeIdle = 5,
+                  kModeIdlePend = 6 };
 /* Deferred hit stores: a lane whose ray is done keeps its (t, primitive) record in registers (kModeIdlePend, an idle
  * lane) and the wave writes the records when it next refills, or at its exit. On gfx9 a store counts in vmcnt, and the
  * loop's in-order vmcnt waits (the pop's, the node fetch's) would otherwise wait for it on the next iteration.
@@ -266,12 +275,12 @@ __device__ __forceinline__ void cursor_from(uint32_t left, uint32_t count, const
  * whose table flags allow packed stack refs, 24-bit record offsets and buffer-resource node loads (the host checks
  * them), so the loop carries no branches for the other layouts; 3 the same with one fetch round per iteration
  * (wf_fetch_once). */
-template <bool COUNT, bool DIAG, int GEO, int LDSN>
-__global__ __launch_bounds__(64, GEO >= 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_simd(LDSN)) void wf_trace(const wcpt_scene_data sd,
-                                                  const wcpt_draw_command* __restrict__ draws,
-                                                  const uint64_t* __restrict__ tri_records, WfBuffers b,
-                                                  uint32_t* __restrict__ status, unsigned long long* __restrict__ counters,
-                                                  uint32_t refill)
+template <bool COUNT, bool DIAG, int GEO, int LDSN, bool PERSIST = false>
+__global__ __launch_bounds__(64, PERSIST ? WCPT_WF_PERSIST_WAVES : (GEO >= 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_simd(LDSN)))
+void wf_trace(const wcpt_scene_data sd, const wcpt_draw_command* __restrict__ draws,
+              const uint64_t* __restrict__ tri_records, WfBuffers b, uint32_t* __restrict__ status,
+              unsigned long long* __restrict__ counters, uint32_t refill, const wcpt_material* __restrict__ mats,
+              const wcpt_sphere* __restrict__ spheres, float4* __restrict__ image, uint32_t W, uint32_t H)
 {
     __shared__ uint64_t s_stack[LDSN * 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.count_out = 0; /* shade appends to it after this kernel */
@@ -546,7 +555,9 @@ __global__ __launch_bounds__(64, GEO >= 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
             }
             if (mode == kModeDone) {
                 /* Intersect result; wf_shade rebuilds the winner's normal and material (:204-208) */
-                if (WCPT_WF_DEFER_HIT) {
+                if (PERSIST) {
+                    mode = kModeShade;
+                } else if (WCPT_WF_DEFER_HIT) {
                     mode = kModeIdlePend;
                 } else {
                     b.hit[p] = make_float4(rt, __uint_as_float(prim), __uint_as_float(primDraw), 0.0f);
@@ -555,6 +566,55 @@ __global__ __launch_bounds__(64, GEO >= 2 ? WCPT_WF_GEO2_WAVES : wf_waves_per_si
                 ref_segment_end<COUNT>(cnt);
             }
             diag_mark<DIAG>(tim, tprev, 4);
+            if (PERSIST) {
+                const unsigned long long sh = __ballot(mode == kModeShade);
+                if (sh && ((uint32_t)__popcll(sh) >= refill || !__ballot(mode < kModeDone)) && mode == kModeShade) {
+                    /* wf_shade's per-path step (:248-280, :309-323) for this lane's path at slot p, one sample */
+                    const float4 r1 = b.in.ray1[p], li = b.in.light[p], tr = b.in.trans[p];
+                    const uint32_t pix = b.in.pix[p];
+                    PathState ps;
+                    ps.ray = ray;
+                    ps.totalLight = mk3(li.x, li.y, li.z);
+                    ps.transmittance = mk3(tr.x, tr.y, tr.z);
+                    ps.bounce = __float_as_uint(r1.z);
+                    uint32_t sample = __float_as_uint(r1.w), seed = __float_as_uint(li.w);
+                    const Hit h = resolve_hit(ps.ray, rt, prim, primDraw, spheres, draws, tri_records);
+                    f3 L;
+                    if (!path_shade(ps, h, seed, sd, mats, L, sample + 1u == sd.samples)) {
+                        float rt0 = kInfinity;
+                        uint32_t prim0 = kNoPrim;
+                        segment_prologue<COUNT>(ps.ray, sd, spheres, rt0, prim0, cnt);
+                        b.in.ray1[p] = make_float4(ps.ray.direction.y, ps.ray.direction.z, __uint_as_float(ps.bounce),
+                                                   __uint_as_float(sample));
+                        b.in.light[p] = make_float4(ps.totalLight.x, ps.totalLight.y, ps.totalLight.z, __uint_as_float(seed));
+                        b.in.trans[p] = make_float4(ps.transmittance.x, ps.transmittance.y, ps.transmittance.z, 0.0f);
+                        ray = ps.ray;
+                        rt = rt0;
+                        prim = prim0;
+                        any = WCPT_LAST_SEGMENT_SHORTCUT && ps.bounce + 1u > sd.maxBounceCount && sample + 1u == sd.samples;
+                        d = 0;
+                        start_draw();
+                    } else {
+                        const float4 rs = b.result[pix];
+                        f3 result = mk3(rs.x, rs.y, rs.z) + L;                  /* :310 */
+                        result = result / (float)sd.samples;                      /* :312 (one sample) */
+                        const uint32_t lx = pix % W, ly = pix / W;
+                        float4* px = image + (size_t)ly * W + lx;
+                        f3 acc;
+                        if (sd.renderedFramesCount == 0) {
+                            acc = result;
+                        } else {
+                            const float4 o = *px;
+                            const float weight = 1.0f / (float)(sd.renderedFramesCount + 1u);
+                            const float iw = 1.0f - weight;
+                            acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight,
+                                      o.z * iw + result.z * weight);
+                        }
+                        store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, acc); /* :323 */
+                        mode = kModeIdle;
+                    }
+                }
+            }
         }
     }
     if (WCPT_WF_DEFER_HIT && mode == kModeIdlePend)
@@ -857,7 +917,7 @@ static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace
                          hipStream_t stream)
 {
     hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, GEO, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
-                       a.tri_records, b, a.status, a.counters, a.wf_refill);
+                       a.tri_records, b, a.status, a.counters, a.wf_refill, a.materials, a.spheres, a.image, a.W, a.H);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
                        a.spheres, a.draws, a.tri_records, b, a.image, a.W, a.H, a.y0, a.counters);
 }
@@ -876,6 +936,24 @@ static hipError_t wf_variant(bool query, int& bpc, const LaunchArgs& a, const Wf
     if (query) return trace_blocks_per_cu<COUNT, DIAG, GEO, LDSN>(bpc);
     wf_iteration<COUNT, DIAG, GEO, LDSN>(a, b, trace_grid, shade_grid, stream);
     return hipGetLastError();
+}
+
+/* The path-persistent trace (PERSIST): one launch for every segment of the pipeline's paths; GEO 2 or 3. */
+template <int GEO>
+static hipError_t wf_persist_variant(bool query, int& bpc, const LaunchArgs& a, const WfBuffers& b, uint32_t grid,
+                                     hipStream_t stream)
+{
+    if (query)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<false, false, GEO, 10, true>, 64, 0);
+    hipLaunchKernelGGL((dev::wf_trace<false, false, GEO, 10, true>), dim3(grid), dim3(64), 0, stream, a.sd, a.draws,
+                       a.tri_records, b, a.status, a.counters, a.wf_refill, a.materials, a.spheres, a.image, a.W, a.H);
+    return hipGetLastError();
+}
+static hipError_t wf_persist_dispatch(int geo, bool query, int& bpc, const LaunchArgs& a, const WfBuffers& b,
+                                      uint32_t grid, hipStream_t stream)
+{
+    return geo == 3 ? wf_persist_variant<3>(query, bpc, a, b, grid, stream)
+                    : wf_persist_variant<2>(query, bpc, a, b, grid, stream);
 }
 
 static hipError_t wf_dispatch(int mode, int geo, int ldsn, bool query, int& bpc, const LaunchArgs& a,
@@ -978,7 +1056,7 @@ static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const Wf
 
 static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32_t pipe, uint32_t npipes,
                                bool sort_rays, int ldsn, int cus, uint32_t trace_grid, uint32_t shade_grid,
-                               hipStream_t stream, WfBuffers b)
+                               uint32_t persist_grid, hipStream_t stream, WfBuffers b)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tiles = tilesX * ((a.rows + 7u) / 8u);
@@ -987,6 +1065,10 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
     /* one draw: the reference's case (PathTracingRenderer.jai:251) */
     const int geo = wf_trace_geo(a, mode, ldsn, P, trace_grid);
     hipError_t e = hipSuccess;
+    if (persist_grid) { /* every segment in one launch (wf_persist_ok) */
+        int unused = 0;
+        return wf_persist_dispatch(geo, false, unused, a, b, persist_grid, stream);
+    }
     /* each iteration advances every live path by one traced segment; a path needs <= samples*(maxBounce+1), or
      * with the primary records reused (wf_shade) maxBounce+1 for sample 0 and maxBounce for each later sample */
     uint64_t iters = (uint64_t)a.sd.samples * ((uint64_t)a.sd.maxBounceCount + 1ull);
@@ -1056,13 +1138,28 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
      * pipelines; 5/8 or 3/4 of the slots per pipeline measured equal, 7/16 slower) */
     if (K > 1) trace_grid = trace_grid / K > 0 ? trace_grid / K : 1u;
 #endif
+    /* the path-persistent trace (WCPT_OPTION_WF_PERSIST): one sample per pixel on the fast layout, and by default only
+     * where every path of a pipeline has a resident lane from the start (row blocks): there the per-bounce launches
+     * each last as long as their slowest ray, and one launch that lets each path run on lasts as long as its slowest
+     * path */
+    uint32_t persist_grid = 0;
+    if (mode == kModeRender && geo == 2 && a.sd.samples == 1u && !sort_rays && a.wf_persist != 0) {
+        if (s0.persist_bpc == 0) {
+            e = wf_persist_dispatch(2, true, s0.persist_bpc, a, WfBuffers{}, 0, stream);
+            if (e != hipSuccess) return e;
+            if (s0.persist_bpc < 1) s0.persist_bpc = 1;
+        }
+        const uint32_t pg = max(1u, (uint32_t)(s0.persist_bpc * cus) / K);
+        const uint64_t per_pipe = ((uint64_t)a.W * a.rows + K - 1) / K;
+        if (a.wf_persist > 0 || per_pipe <= 64ull * pg) persist_grid = pg;
+    }
     e = wf_reserve_result(w, (uint64_t)a.W * a.rows);
     if (e != hipSuccess) return e;
     WfBuffers bs[kWfMaxPipes];
     if (K == 1) {
         e = pipe_begin(a, mode, s0, s0, w.result, w.result + w.result_capacity, 0, 1, cus, stream, bs[0]);
         if (e != hipSuccess) return e;
-        return pipe_iterate(a, mode, s0, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, stream, bs[0]);
+        return pipe_iterate(a, mode, s0, 0, 1, sort_rays, ldsn, cus, trace_grid, shade_grid, persist_grid, stream, bs[0]);
     }
 
     /* fork: pipelines 1..K-1 run on their own streams after everything already queued on the context's stream */
@@ -1104,7 +1201,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
                 if (i != j) first = hipStreamWaitEvent(j == 0 ? stream : w.aux[j], w.ready[i], 0);
     }
     for (uint32_t j = 0; j < K && first == hipSuccess; j++)
-        first = pipe_iterate(a, mode, w.pipe[j], j, K, false, ldsn, cus, trace_grid, shade_grid,
+        first = pipe_iterate(a, mode, w.pipe[j], j, K, false, ldsn, cus, trace_grid, shade_grid, persist_grid,
                              j == 0 ? stream : w.aux[j], bs[j]);
     /* join: the context's stream continues after every pipeline (also after a failed enqueue) */
     for (uint32_t j = 1; j < K; j++) {

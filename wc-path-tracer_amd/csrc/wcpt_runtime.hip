@@ -153,6 +153,7 @@ struct wcpt_context {
     int tri_cache = 1;                 /* WCPT_OPTION_TRIANGLE_CACHE */
     int packed_refs = 1;               /* WCPT_OPTION_PACKED_REFS */
     int wf_fetch = -1;                 /* WCPT_OPTION_WF_FETCH */
+    int wf_persist = -1;               /* WCPT_OPTION_WF_PERSIST */
     int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (round 5 with the deferred hit stores, c4: 8 / 12 / 16 / 20 / 24 / 32 -> 203.5 / 199.6 / 198.9 / 198.0 / 198.6 / 201.4 ms; c3 flat; profiles/r05_fetch_once_ab.log) */
 #ifndef WCPT_WF_PIPES_DEFAULT
 #define WCPT_WF_PIPES_DEFAULT 0
@@ -552,6 +553,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.wf_fast = false;
     a.wf_refill = (uint32_t)ctx->wf_refill;
     a.wf_fetch = ctx->wf_fetch;
+    a.wf_persist = ctx->wf_persist;
     a.mk_tile_order = (uint32_t)ctx->mk_tile_order;
     hipEvent_t e0 = nullptr, e1 = nullptr;
 /* Profiling events time the launches only: no system-scope fence when they are recorded (hip_runtime_api.h,
@@ -878,6 +880,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         return WCPT_SUCCESS;
     case WCPT_OPTION_DIAGNOSTICS:
         ctx->diagnostics = value ? 1 : 0;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_WF_PERSIST:
+        if (value < -1 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wavefront persist %d", value);
+        ctx->wf_persist = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_WF_FETCH:
         if (value < -1 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wavefront fetch rounds %d", value);

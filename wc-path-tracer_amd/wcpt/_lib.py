@@ -54,6 +54,7 @@ OPTION_MK_TILE_ORDER = 9
 OPTION_WF_PIPES = 10
 OPTION_PROFILE_REGION = 11
 OPTION_WF_FETCH = 12
+OPTION_WF_PERSIST = 13
 DEFAULT_WF_PIPES = 0  # wcpt_runtime.hip: by queue length (2 or 3)
 
 # gather payload formats (wcpt_set_gather_output, wcpt_group_set_output)
