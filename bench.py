@@ -368,6 +368,8 @@ def parse_args(argv=None):
                     help="WCPT_OPTION_WF_REFILL: idle lanes before a trace wave refetches (0: the library default)")
     ap.add_argument("--wf-fetch", type=int, default=-1, choices=[-1, 0, 1],
                     help="WCPT_OPTION_WF_FETCH: wavefront trace fetch rounds per iteration (-1: the library's choice)")
+    ap.add_argument("--wf-persist", type=int, default=-1, choices=[-1, 0, 1],
+                    help="WCPT_OPTION_WF_PERSIST: the path-persistent wavefront trace (-1: the library's choice)")
     ap.add_argument("--wf-pipes", type=int, default=0,
                     help="wavefront kernel: concurrent pipelines (WCPT_OPTION_WF_PIPES; 0 = the library default)")
     ap.add_argument("--camera", default="still", choices=["still", "orbit"],
@@ -526,6 +528,8 @@ class GroupBench:
                 c.set_option(T.OPTION_WF_REFILL, args.wf_refill)
             if args.wf_fetch >= 0:
                 c.set_option(T.OPTION_WF_FETCH, args.wf_fetch)
+            if args.wf_persist >= 0:
+                c.set_option(T.OPTION_WF_PERSIST, args.wf_persist)
             self.devs.append(wcpt.DeviceScene(c, scene))
         self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
         if getattr(args, "group_threads", None) is not None:
@@ -644,6 +648,8 @@ class TorchBench:
             self.ctx.set_option(wcpt._lib.OPTION_WF_REFILL, args.wf_refill)
         if args.wf_fetch >= 0:
             self.ctx.set_option(wcpt._lib.OPTION_WF_FETCH, args.wf_fetch)
+        if args.wf_persist >= 0:
+            self.ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, args.wf_persist)
         self.dev = wcpt.DeviceScene(self.ctx, scene)
         self.ctx.create_screen(W, H)
         y0, rows = row_block(H, self.world, self.rank)
