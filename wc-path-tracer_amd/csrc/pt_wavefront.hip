@@ -119,13 +119,16 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 #ifndef WCPT_WF_LEAF_RECORDS
 #define WCPT_WF_LEAF_RECORDS 1 /* the fast layout also requires kTriFlagLeafRecords: leaf steps need no index path */
 #endif
-/* Path-persistent trace (PERSIST instances, wf_persist_ok): one launch runs every segment of its paths. A lane whose
+/* Path-persistent trace (PERSIST instances, launch_wavefront): one launch runs every segment of its paths. A lane whose
  * ray is done shades it in place (resolve_hit, path_shade, the next segment's sphere loop, or the pixel's store) and
  * goes on with the path's next segment, so no path waits for the slowest ray of its bounce; the wave shades once
  * `refill` of its lanes wait, or when none is tracing. Used where a pipeline's queue is short (row blocks), for one
  * sample per pixel. */
 #ifndef WCPT_WF_PERSIST_WAVES
 #define WCPT_WF_PERSIST_WAVES 4
+#endif
+#ifndef WCPT_WF_PERSIST_GEO
+#define WCPT_WF_PERSIST_GEO 3 /* the persistent trace's fetch rounds: 3 one per iteration, 2 two */
 #endif
 #ifndef WCPT_WF_GEO2_WAVES
 #define WCPT_WF_GEO2_WAVES 8 /* occupancy floor of the fast-layout trace (waves per SIMD) */
@@ -1065,9 +1068,9 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
     /* one draw: the reference's case (PathTracingRenderer.jai:251) */
     const int geo = wf_trace_geo(a, mode, ldsn, P, trace_grid);
     hipError_t e = hipSuccess;
-    if (persist_grid) { /* every segment in one launch (wf_persist_ok) */
+    if (persist_grid) { /* every segment in one launch (launch_wavefront) */
         int unused = 0;
-        return wf_persist_dispatch(geo, false, unused, a, b, persist_grid, stream);
+        return wf_persist_dispatch(WCPT_WF_PERSIST_GEO, false, unused, a, b, persist_grid, stream);
     }
     /* each iteration advances every live path by one traced segment; a path needs <= samples*(maxBounce+1), or
      * with the primary records reused (wf_shade) maxBounce+1 for sample 0 and maxBounce for each later sample */
@@ -1124,11 +1127,27 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     const uint32_t shade_grid = WCPT_SHADE_BLOCKS_PER_CU > 0 ? (uint32_t)(cus * WCPT_SHADE_BLOCKS_PER_CU)
                                                              : (P + dev::kShadeBlock - 1) / dev::kShadeBlock;
     sort_rays = sort_rays && a.sd.drawCommandCount > 0;
-    /* pipelines: the option's count, or (0, the default) 3 when the frame holds at most 8 paths per resident trace lane
-     * -- the launches are short and their tails weigh, so a third chain overlaps them (c3 4.41-4.46 against 4.50-4.55
-     * ms with two) -- and 2 on longer queues (c4 199.5 against 197.9 ms with two; profiles/r05_pipes_ab.log) */
+    /* the path-persistent trace (WCPT_OPTION_WF_PERSIST): one sample per pixel on the fast layout, and by default only
+     * where every path of the frame has a resident lane of it from the start (row blocks): there the per-bounce
+     * launches each last as long as their slowest ray, and one launch that lets each path run on lasts as long as its
+     * slowest path (c3 135-row blocks 1.30 against 1.85 ms; the full c3 frame 6.64 against 4.55 ms,
+     * profiles/r05_persist_ab.log) */
+    const bool persist_ok = mode == kModeRender && geo == 2 && a.sd.samples == 1u && !sort_rays && a.wf_persist != 0;
+    if (persist_ok && s0.persist_bpc == 0) {
+        e = wf_persist_dispatch(WCPT_WF_PERSIST_GEO, true, s0.persist_bpc, a, WfBuffers{}, 0, stream);
+        if (e != hipSuccess) return e;
+        if (s0.persist_bpc < 1) s0.persist_bpc = 1;
+    }
+    const uint32_t persist_full = persist_ok ? (uint32_t)(s0.persist_bpc * cus) : 0u;
+    const bool persist = persist_ok && (a.wf_persist > 0 || (uint64_t)a.W * a.rows <= 64ull * persist_full);
+    /* pipelines: the option's count, or (0, the default) one for the path-persistent trace (its blocks measured 1.30 /
+     * 1.40 / 1.40 ms with 1 / 2 / 3), else 3 when the frame holds at most 8 paths per resident trace lane -- the
+     * launches are short and their tails weigh, so a third chain overlaps them (c3 4.41-4.46 against 4.50-4.55 ms with
+     * two) -- and 2 on longer queues (c4 199.5 against 197.9 ms with two; profiles/r05_pipes_ab.log) */
     uint32_t K = (uint32_t)(pipes > kWfMaxPipes ? kWfMaxPipes : pipes);
-    if (pipes < 1) K = (uint64_t)a.W * a.rows <= (uint64_t)WCPT_WF_FETCH_ONCE_RATIO * 64ull * trace_grid ? 3u : 2u;
+    if (pipes < 1) {
+        K = persist ? 1u : ((uint64_t)a.W * a.rows <= (uint64_t)WCPT_WF_FETCH_ONCE_RATIO * 64ull * trace_grid ? 3u : 2u);
+    }
     if (sort_rays || mode == kModeDiag) K = 1; /* one sort scratch and one diagnostics block */
     const uint32_t tiles = tilesX * tilesY;
     if (K > tiles) K = tiles;
@@ -1138,21 +1157,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
      * pipelines; 5/8 or 3/4 of the slots per pipeline measured equal, 7/16 slower) */
     if (K > 1) trace_grid = trace_grid / K > 0 ? trace_grid / K : 1u;
 #endif
-    /* the path-persistent trace (WCPT_OPTION_WF_PERSIST): one sample per pixel on the fast layout, and by default only
-     * where every path of a pipeline has a resident lane from the start (row blocks): there the per-bounce launches
-     * each last as long as their slowest ray, and one launch that lets each path run on lasts as long as its slowest
-     * path */
-    uint32_t persist_grid = 0;
-    if (mode == kModeRender && geo == 2 && a.sd.samples == 1u && !sort_rays && a.wf_persist != 0) {
-        if (s0.persist_bpc == 0) {
-            e = wf_persist_dispatch(2, true, s0.persist_bpc, a, WfBuffers{}, 0, stream);
-            if (e != hipSuccess) return e;
-            if (s0.persist_bpc < 1) s0.persist_bpc = 1;
-        }
-        const uint32_t pg = max(1u, (uint32_t)(s0.persist_bpc * cus) / K);
-        const uint64_t per_pipe = ((uint64_t)a.W * a.rows + K - 1) / K;
-        if (a.wf_persist > 0 || per_pipe <= 64ull * pg) persist_grid = pg;
-    }
+    const uint32_t persist_grid = persist ? max(1u, persist_full / K) : 0u;
     e = wf_reserve_result(w, (uint64_t)a.W * a.rows);
     if (e != hipSuccess) return e;
     WfBuffers bs[kWfMaxPipes];
