@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--wf-pipes", type=int, default=0, help="WCPT_OPTION_WF_PIPES (0: the library default)")
     ap.add_argument("--wf-fetch", type=int, default=-1, help="WCPT_OPTION_WF_FETCH (-1: auto)")
     ap.add_argument("--wf-persist", type=int, default=-1, help="WCPT_OPTION_WF_PERSIST (-1: auto)")
+    ap.add_argument("--wf-refill", type=int, default=0, help="WCPT_OPTION_WF_REFILL (0: the library default)")
     ap.add_argument("--skip-full", action="store_true", help="do not time the full frame (full/N columns then 0)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
@@ -43,6 +44,8 @@ def main():
         ctx.set_option(wcpt._lib.OPTION_WF_PIPES, a.wf_pipes)
     ctx.set_option(wcpt._lib.OPTION_WF_FETCH, a.wf_fetch)
     ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, a.wf_persist)
+    if a.wf_refill:
+        ctx.set_option(wcpt._lib.OPTION_WF_REFILL, a.wf_refill)
     dev = wcpt.DeviceScene(ctx, s)
     ctx.create_screen(W, H)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
