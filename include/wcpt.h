@@ -122,8 +122,8 @@ extern "C" {
  * (issue-bound). Same results. */
 #define WCPT_OPTION_WF_FETCH 12
 /* Wavefront: the path-persistent trace, one launch per frame in which each lane runs its path's segments one after
- * another and shades between them, for one sample per pixel on one-draw scenes. -1 (default): where every path of a
- * pipeline has a resident lane from the start (row blocks), 0 never, 1 whenever eligible. Same results. */
+ * another and shades between them, for one sample per pixel on one-draw scenes. -1 (default): where the frame has at
+ * most 1.4 paths per resident lane of it (row blocks), 0 never, 1 whenever eligible. Same results. */
 #define WCPT_OPTION_WF_PERSIST 13
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */

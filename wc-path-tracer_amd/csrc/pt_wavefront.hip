@@ -1128,7 +1128,7 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
                                                              : (P + dev::kShadeBlock - 1) / dev::kShadeBlock;
     sort_rays = sort_rays && a.sd.drawCommandCount > 0;
     /* the path-persistent trace (WCPT_OPTION_WF_PERSIST): one sample per pixel on the fast layout, and by default only
-     * where every path of the frame has a resident lane of it from the start (row blocks): there the per-bounce
+     * where the frame's paths about fit its resident lanes (row blocks): there the per-bounce
      * launches each last as long as their slowest ray, and one launch that lets each path run on lasts as long as its
      * slowest path (c3 135-row blocks 1.30 against 1.85 ms; the full c3 frame 6.64 against 4.55 ms,
      * profiles/r05_persist_ab.log) */
@@ -1139,7 +1139,9 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
         if (s0.persist_bpc < 1) s0.persist_bpc = 1;
     }
     const uint32_t persist_full = persist_ok ? (uint32_t)(s0.persist_bpc * cus) : 0u;
-    const bool persist = persist_ok && (a.wf_persist > 0 || (uint64_t)a.W * a.rows <= 64ull * persist_full);
+    /* at most 1.4 paths per resident lane: the lanes freed by the first paths take the rest (7- / 6-way c3 splits at
+     * 1.13 / 1.32 paths per lane gain 7 % / 3 %, 5-way at 1.58 is flat, 4-way at 2.0 loses) */
+    const bool persist = persist_ok && (a.wf_persist > 0 || (uint64_t)a.W * a.rows * 5ull <= 64ull * 7ull * persist_full);
     /* pipelines: the option's count, or (0, the default) one for the path-persistent trace (its blocks measured 1.30 /
      * 1.40 / 1.40 ms with 1 / 2 / 3), else 3 when the frame holds at most 8 paths per resident trace lane -- the
      * launches are short and their tails weigh, so a third chain overlaps them (c3 4.41-4.46 against 4.50-4.55 ms with
