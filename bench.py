@@ -257,15 +257,18 @@ def _cgroup_cpu_quota():
 
 
 def baseline_threads(cpu_count=None, affinity=None, quota="read") -> dict:
-    """The CPU baseline's thread counts. BASELINE.md:21 and SURVEY §8(d): the port on ALL host cores, i.e. one thread per
-    logical CPU the host reports (os.cpu_count(); the oracle takes at most 1024). Beside it, clearly labelled, the
-    per-GPU share of an 8-GPU node's host: 16 threads (the GPU box's CPU share per GPU). Also reported: the CPUs this
-    process may run on (sched_getaffinity) and the cgroup quota, since a container may see more CPUs than it may use."""
+    """The CPU baseline's thread count: one thread per CPU this process can actually use (BASELINE.md:21, SURVEY
+    §8(d): the port on all host cores), i.e. min(logical CPUs the host reports, CPUs in this process's affinity mask,
+    the cgroup CPU quota rounded up). A container may see many more CPUs than its quota lets it run: threads beyond
+    the quota only time-slice (256 threads under a 16-CPU quota measured 1.56x below 16 threads).
+    Beside it, labelled, the 16-thread per-GPU share of an 8-GPU node's host when that differs."""
+    import math
     n = cpu_count if cpu_count is not None else (os.cpu_count() or 1)
     if affinity is None:
         affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else n
     q = _cgroup_cpu_quota() if quota == "read" else quota
-    return {"threads": max(1, min(n, 1024)), "share_threads": max(1, min(16, n)), "logical_cpus": n,
+    usable = max(1, min(n, affinity, math.ceil(q) if q else n, 1024))
+    return {"threads": usable, "share_threads": max(1, min(16, usable)), "logical_cpus": n,
             "affinity_cpus": affinity, "cgroup_cpu_quota": q}
 
 
@@ -324,24 +327,25 @@ def _cpu_rate(scene, width, height, spp, bounces, threads, budget_s, min_frames)
 
 def cpu_baseline(scene, width, height, spp, bounces, budget_s=20.0, min_frames=5):
     """The CPU oracle (a scalar C restatement of pathTracer.comp, oracle/pt_oracle.c, built -O3 -march=native on this
-    host; rows claimed dynamically by its threads) on all host cores (baseline_threads: one thread per logical CPU,
-    BASELINE.md:21), and beside it on the 16-thread per-GPU share. ~60 % of budget_s goes to the all-core figure
-    (`value`), the rest to the share (`per_gpu_share`)."""
+    host; rows claimed dynamically by its threads) on every CPU this process can use (baseline_threads, BASELINE.md:21),
+    and beside it on the 16-thread per-GPU share when that differs (then ~60 % of budget_s goes to `value`, the rest to
+    `per_gpu_share`)."""
     lib, flags = _native_oracle()
     os.environ["WCPT_ORACLE_LIB"] = lib
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     th = baseline_threads()
     where = f"{_cpu_model()}, oracle/pt_oracle.c built {flags} (lavapipe is not available)"
-    allc = _cpu_rate(scene, width, height, spp, bounces, th["threads"], 0.6 * budget_s, min_frames)
+    split = th["share_threads"] != th["threads"]
+    allc = _cpu_rate(scene, width, height, spp, bounces, th["threads"], (0.6 if split else 1.0) * budget_s, min_frames)
     out = {"value": allc["value"], "unit": "Mray/s", "cores": th["threads"], "kind": "port",
-           "sample": f"{allc['sample']} on {th['threads']} threads (all {th['logical_cpus']} logical CPUs the host "
-                     f"reports; this process may run on {th['affinity_cpus']}, cgroup quota "
-                     f"{th['cgroup_cpu_quota'] or 'none'}) of {where}",
+           "sample": f"{allc['sample']} on {th['threads']} threads (the CPUs this process can use: "
+                     f"{th['logical_cpus']} logical CPUs reported, {th['affinity_cpus']} in its affinity mask, cgroup "
+                     f"quota {th['cgroup_cpu_quota'] or 'none'}) of {where}",
            "logical_cpus": th["logical_cpus"], "affinity_cpus": th["affinity_cpus"],
            "cgroup_cpu_quota": th["cgroup_cpu_quota"]}
     if "frame_ms_median" in allc:
         out["frame_ms_median"] = allc["frame_ms_median"]
-    if th["share_threads"] != th["threads"]:
+    if split:
         sh = _cpu_rate(scene, width, height, spp, bounces, th["share_threads"], 0.4 * budget_s, min_frames)
         out["per_gpu_share"] = {"value": sh["value"], "unit": "Mray/s", "cores": th["share_threads"],
                                 "label": "16 threads: one GPU's share of an 8-GPU node's host (not the baseline)",
@@ -422,7 +426,93 @@ def parse_args(argv=None):
                     help="under torchrun: rccl (default) = the product's one-process-per-device group over RCCL, no "
                          "torch; gloo / gloo-host / torch-nccl = the torch.distributed gather (gloo rehearses N ranks "
                          "on one GPU, where RCCL refuses two ranks on one device)")
+    ap.add_argument("--one-process", action="store_true",
+                    help="N > 1 without a launcher: drive every rank from this one process and thread "
+                         "(wcpt_group_create_ex; RCCL ncclCommInitAll) instead of spawning one process per GPU. With "
+                         "RCCL over several GPUs this form has never run on hardware, and the line says so")
+    ap.add_argument("--group-timeout-ms", type=int, default=None,
+                    help="WCPT_GROUP_OPTION_TIMEOUT_MS: how long wcpt_group_sync waits for a frame's exchange before "
+                         "it aborts the communicator and returns WCPT_ERROR_DEVICE_LOST (default: the library's; "
+                         "0 = wait forever)")
     return ap.parse_args(argv)
+
+
+def launch_plan(args, env) -> str:
+    """How this invocation runs its ranks, decided before anything touches the GPU:
+      "ranks"  -- under a launcher (WORLD_SIZE set): this process is one rank of a one-process-per-GPU group;
+      "spawn"  -- plain `python bench.py --gpus N` (N > 1, RCCL): this process spawns N fresh rank processes, each
+                  running the one-process-per-GPU path that torchrun runs (wcpt_group_create_rank), and waits for them;
+      "group"  -- one process drives every rank (N = 1; or --one-process, --transport copy|direct, --devices)."""
+    if int(env.get("WORLD_SIZE", "1")) > 1:
+        return "ranks"
+    n = 1 if args.gpus is None else args.gpus
+    if n > 1 and not args.one_process and args.transport == "rccl" and not args.devices:
+        return "spawn"
+    return "group"
+
+
+def _free_tcp_port(addr: str = "127.0.0.1") -> int:
+    import socket
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    try:
+        s.bind((addr, 0))
+        return s.getsockname()[1]
+    finally:
+        s.close()
+
+
+def spawn_env(env, n: int, rank: int, port: int, run_id: str) -> dict:
+    """The environment of spawned rank `rank` of `n`: what torchrun gives its workers (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR/PORT, a run id for the rendezvous token), plus WCPT_BENCH_LAUNCH=spawn so the line
+    names the launch."""
+    e = dict(env)
+    e.update(WORLD_SIZE=str(n), RANK=str(rank), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+             MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_RUN_ID=run_id, WCPT_BENCH_LAUNCH="spawn")
+    return e
+
+
+def spawn_ranks(argv, n: int, env=None, child_cmd=None, timeout_s: float = 0.0, poll_s: float = 0.05) -> int:
+    """Run `n` rank processes of this bench (the same argv; each sees WORLD_SIZE = n) and wait for them. The parent
+    never loads libwcpt or touches a GPU, and never execs: every rank is a fresh child process (subprocess), which
+    inherits stdout/stderr, so rank 0's JSON line is this command's output. When a rank fails, the others are
+    terminated (they would wait for its exchange); returns 0, the first failing rank's exit status (128 + signal for a
+    signalled one), or 3 when the ranks outlive `timeout_s`."""
+    import secrets
+    import subprocess
+    env = dict(os.environ if env is None else env)
+    cmd = list(child_cmd) if child_cmd else [sys.executable, os.path.abspath(__file__)]
+    port = _free_tcp_port()
+    run_id = f"wcpt-spawn-{os.getpid()}-{secrets.token_hex(4)}"
+    procs = []
+    try:
+        for r in range(n):
+            procs.append(subprocess.Popen(cmd + list(argv), env=spawn_env(env, n, r, port, run_id)))
+        deadline = time.monotonic() + timeout_s if timeout_s and timeout_s > 0 else None
+        rc = 0
+        while [p.poll() for p in procs].count(None):      # poll every rank (any() would stop at the first)
+            bad = [p for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                sys.stderr.write(f"bench.py: rank {procs.index(bad[0])} exited with {rc}; stopping the other ranks\n")
+                break
+            if deadline is not None and time.monotonic() > deadline:
+                sys.stderr.write(f"bench.py: spawned ranks still running after {timeout_s:.0f} s; stopping them\n")
+                rc = 3
+                break
+            time.sleep(poll_s)
+        else:
+            rc = next((p.returncode for p in procs if p.returncode), 0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return 128 - rc if rc < 0 else rc
 
 
 def resolve_topology(args, env) -> dict:
@@ -432,8 +522,8 @@ def resolve_topology(args, env) -> dict:
         if args.gpus is not None and args.gpus != world:
             raise SystemExit(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}: one rank per "
                              f"GPU, so they must agree")
-        if args.devices:
-            raise SystemExit("bench.py: --devices is for the one-process group (no WORLD_SIZE)")
+        if args.devices or args.one_process:
+            raise SystemExit("bench.py: --devices / --one-process are for the one-process group (no WORLD_SIZE)")
         local = int(env.get("LOCAL_RANK", env.get("RANK", "0")))
         if args.rccl_rehearsal and args.dist_backend != "rccl":
             raise SystemExit("bench.py: --rccl-rehearsal rehearses the RCCL group (--dist-backend rccl)")
@@ -534,6 +624,8 @@ class GroupBench:
         self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
         if getattr(args, "group_threads", None) is not None:
             self.g.set_option(T.GROUP_OPTION_THREADS, args.group_threads)
+        if getattr(args, "group_timeout_ms", None) is not None:
+            self.g.set_option(T.GROUP_OPTION_TIMEOUT_MS, args.group_timeout_ms)
         self.g.create_screen(W, H)
         self.fmt, self.px = GATHER_FORMATS[args.gather]
         self.out = None
@@ -844,6 +936,10 @@ def rccl_rehearsal_env(env, rank: int):
 def main(argv=None):
     global wcpt
     args = parse_args(argv)
+    if launch_plan(args, os.environ) == "spawn":
+        # before any GPU call in this process: the ranks are fresh processes (never an exec of this one)
+        wd = args.watchdog_s + 120.0 if args.watchdog_s and args.watchdog_s > 0 else 0.0
+        return spawn_ranks(sys.argv[1:] if argv is None else list(argv), args.gpus, timeout_s=wd)
     topo = resolve_topology(args, os.environ)
     watchdog = _start_watchdog(args.watchdog_s, topo)
     if args.rccl_rehearsal:
@@ -983,6 +1079,7 @@ def main(argv=None):
                                        + ("" if args.no_overlap else " overlapped with the next frame")
                                        if nranks > 1 else "one device")},
             "ranks": nranks,
+            "launch": launch_label(topo["mode"], os.environ),
             "group": {"kind": kind[topo["mode"]], "transport": transport, "rccl_ranks": info["nranks"]
                       if transport == "rccl" else None, "overlap": not args.no_overlap, "devices": topo["devices"]
                       if topo["mode"] == "group" else None},
@@ -1004,6 +1101,10 @@ def main(argv=None):
         }
         if nranks > 1:
             out["per_rank_block_ms"] = [b["block_ms"] for b in blocks]
+            if topo["mode"] == "group" and transport == "rccl" and distinct > 1:
+                out["unrehearsed"] = ("the one-process RCCL group (ncclCommInitAll, every rank issued from one thread) "
+                                      "over several GPUs has never run on hardware before this line; the default "
+                                      "N-GPU command spawns one process per GPU instead")
             if distinct < nranks:
                 out["rehearsal"] = f"{nranks} ranks on {distinct} device(s): not a scaling measurement"
                 if args.rccl_rehearsal:
@@ -1034,6 +1135,15 @@ def main(argv=None):
         watchdog.cancel()
 
 
+def launch_label(mode: str, env) -> str:
+    """Which launch produced this line: bench.py's own rank spawner, an external launcher (torchrun), or one process."""
+    if mode == "group":
+        return "one process (no launcher)"
+    if env.get("WCPT_BENCH_LAUNCH") == "spawn":
+        return "spawned by bench.py: one fresh process per rank (plain --gpus N, no launcher)"
+    return "external launcher (torchrun or equivalent: WORLD_SIZE / RANK / LOCAL_RANK in the environment)"
+
+
 def hip_runtime_label(mode: str) -> str:
     v = wcpt.runtime_version()
     where = ("the system /opt/rocm runtime (torch not imported)" if mode != "torch" else
@@ -1042,4 +1152,4 @@ def hip_runtime_label(mode: str) -> str:
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -375,14 +375,17 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
  *                          host) only for the transfer that last read the payload it rewrites. 0: transfers run on
  *                          the render streams, in line with the renders.
  *   wcpt_group_sync        waits for every local rank's renders and transfers (and reports a traversal-stack
- *                          overflow on any of them). The presented frame is complete after it.
+ *                          overflow on any of them). The presented frame is complete after it. The wait is bounded
+ *                          (WCPT_GROUP_OPTION_TIMEOUT_MS): a frame whose exchange cannot complete (a peer failed or
+ *                          skipped it) ends in WCPT_ERROR_DEVICE_LOST, not in a hang.
  * Errors leave the group usable, except (a) any failure once a frame's device work has started to be issued (a render
  * launch, an event, a transfer: the ranks are then out of step), and (b), in a group created with
  * wcpt_group_create_rank, an error that the other processes cannot have seen -- any wcpt_group_render error while
  * presenting, a check of the root's own `dst` (alignment, a null dst with a nonzero format), a device failure in
  * wcpt_group_create_screen / wcpt_group_set_output -- since the other processes still post their part of the next
  * exchange. The group then aborts its communicators and every later call but wcpt_group_destroy returns
- * WCPT_ERROR_DEVICE_LOST; the other processes' exchange does not complete, and their host ends them. Refusals made
+ * WCPT_ERROR_DEVICE_LOST; the other processes' exchange does not complete, and their wcpt_group_sync returns
+ * WCPT_ERROR_DEVICE_LOST at its timeout (or earlier, on the transport's asynchronous error). Refusals made
  * alike in every process (frame size, format, `bytes`) leave the group usable.
  * wcpt_last_error(wcpt_group_context(g, r)) or wcpt_last_error(NULL) explains an error. */
 /* The row-block split itself, for a host that runs one process per device (then wcpt_set_row_range with the
@@ -400,12 +403,22 @@ typedef struct wcpt_group wcpt_group;
 /* How a one-process group issues a frame to its devices. 1: the caller's thread issues the first local rank's share
  * (validation, render launch, events, transfer) while a host thread per other local rank issues that rank's share at the
  * same time, and wcpt_group_render returns once every share is enqueued (the API stays single-threaded for the caller;
- * threads spin ~0.2 ms between frames, then sleep). 0: the caller's thread issues every rank's share in turn. -1
- * (default): 1 when the group's ranks span more than one device and the transport is COPY or DIRECT, else 0 (an RCCL
- * group issues all its sends and receives inside one ncclGroupStart/End from one thread unless 1 is set). Same device work either way. Host issue per
+ * threads spin ~0.2 ms between frames, then sleep). 0 (default): the caller's thread issues every rank's share in turn.
+ * -1: 1 when the group's ranks span more than one device and the transport is COPY or DIRECT, else 0 (an RCCL group
+ * issues all its sends and receives inside one ncclGroupStart/End from one thread unless 1 is set). Same device work
+ * either way. Off by default because the threaded issue has only run with every rank on one device. Host issue per
  * frame at 8 ranks (measured on one device): COPY 95-137 us in one thread, 28-40 us with threads; DIRECT
  * 27.5 us in one thread, 13.5 us with threads. */
 #define WCPT_GROUP_OPTION_THREADS 2
+/* Bound on one wcpt_group_sync (and on the drain in wcpt_group_destroy), in milliseconds; 0 = wait forever; default
+ * 60000 in a group of several ranks (none in a group of one). The sync polls each local rank's render and
+ * communication streams (hipStreamQuery) and the communicator's asynchronous error (ncclCommGetAsyncError) instead of
+ * blocking: when a peer has failed or did not post its part of a frame's exchange, the transfers never complete, so on
+ * an asynchronous error or at the deadline the group aborts its communicators (ncclCommAbort), lets the aborted work
+ * drain, and returns WCPT_ERROR_DEVICE_LOST (the group is then broken: every later call but wcpt_group_destroy returns
+ * WCPT_ERROR_DEVICE_LOST). Pick it above the longest run of frames the host queues between two syncs. Option 3 was
+ * added under ABI 4. */
+#define WCPT_GROUP_OPTION_TIMEOUT_MS 3
 typedef struct wcpt_group_info {
     int32_t nranks;            /* ranks of the group; RCCL: ncclCommCount of this process's first communicator */
     int32_t local_ranks;       /* ranks driven by this process */

@@ -28,3 +28,33 @@ extern "C" int plan_frames(int nranks, int root, int overlap, int transport, int
     }
     return n;
 }
+
+// The bounded wait of wcpt_group_sync (wc-path-tracer_amd/csrc/group_wait.h) against a stand-in stream and clock: the
+// stream drains after `ready_after` polls (< 0: never), the transport reports an asynchronous error from poll
+// `error_after` on (< 0: never), and a poll fails at `fail_at` (< 0: never). Each poll advances the clock by
+// ms_per_poll, each nap by its length. Returns the wait's result; *elapsed_ms / *polls / *naps say how it got there.
+#include "../wc-path-tracer_amd/csrc/group_wait.h"
+
+extern "C" int wait_sim(int ready_after, int error_after, int fail_at, double timeout_ms, double ms_per_poll,
+                        double* elapsed_ms, int* polls, int* naps)
+{
+    double clock = 1000.0;
+    int n = 0, k = 0;
+    const double t0 = clock;
+    const wcpt::gwait::Result r = wcpt::gwait::wait_for(
+        [&]() {
+            const int i = n++;
+            clock += ms_per_poll;
+            if (fail_at >= 0 && i >= fail_at) return (int)wcpt::gwait::kPollError;
+            return ready_after >= 0 && i >= ready_after ? (int)wcpt::gwait::kReady : (int)wcpt::gwait::kBusy;
+        },
+        [&]() { return error_after >= 0 && n > error_after; }, t0, timeout_ms, [&]() { return clock; },
+        [&](double us) {
+            k++;
+            clock += us / 1000.0;
+        });
+    *elapsed_ms = clock - t0;
+    *polls = n;
+    *naps = k;
+    return (int)r;
+}

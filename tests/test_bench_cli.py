@@ -211,25 +211,33 @@ def test_watchdog_ends_a_hung_run():
 
 
 def test_cpu_baseline_threads_follow_the_plan():
-    """the CPU baseline runs the port on one thread per logical CPU the host reports
-    (BASELINE.md:21, SURVEY 8(d): all host cores), the 16-thread per-GPU share only beside it."""
-    t = bench.baseline_threads(cpu_count=256, affinity=16, quota=16.0)
-    assert t["threads"] == 256 and t["share_threads"] == 16 and t["logical_cpus"] == 256
+    """the CPU baseline runs the port on one thread per CPU the process can actually use --
+    min(logical CPUs reported, affinity mask, cgroup quota rounded up) -- not on every logical CPU a container sees (256
+    threads under a 16-CPU quota only time-slice). The 16-thread per-GPU share is reported beside it when it differs."""
+    t = bench.baseline_threads(cpu_count=256, affinity=256, quota=16.0)      # the GPU box: 256 logical, quota 16
+    assert t["threads"] == 16 and t["share_threads"] == 16 and t["logical_cpus"] == 256
+    assert bench.baseline_threads(cpu_count=256, affinity=24, quota=None)["threads"] == 24
+    assert bench.baseline_threads(cpu_count=64, affinity=64, quota=12.5)["threads"] == 13
+    t = bench.baseline_threads(cpu_count=64, affinity=64, quota=None)
+    assert t["threads"] == 64 and t["share_threads"] == 16
     assert bench.baseline_threads(cpu_count=4, affinity=4, quota=None)["share_threads"] == 4
     assert bench.baseline_threads(cpu_count=4096, affinity=4096, quota=None)["threads"] == 1024  # the oracle's cap
     here = bench.baseline_threads()
-    assert here["threads"] == min(os.cpu_count(), 1024)
+    q = bench._cgroup_cpu_quota()
+    assert here["threads"] == max(1, min(os.cpu_count(), len(os.sched_getaffinity(0)), 1024,
+                                         -(-int(q * 100) // 100) if q else 1024))
 
 
-def test_cpu_baseline_runs_on_all_cores():
-    """The baseline leg itself on a small workload: cores = the host's logical CPUs, a positive rate, and the share
-    figure labelled beside it when the host has more than 16 CPUs."""
+def test_cpu_baseline_runs_on_the_usable_cores():
+    """The baseline leg itself on a small workload: cores = the CPUs this process can use, a positive rate, and the
+    share figure labelled beside it only when that differs from 16."""
     sys.path.insert(0, os.path.join(ROOT, "wc-path-tracer_amd"))
     from wcpt import scene as wscene
     s = wscene.generate("cornell")
+    th = bench.baseline_threads()
     cb = bench.cpu_baseline(s, 64, 64, 1, 1, budget_s=1.0, min_frames=2)
-    assert cb["cores"] == min(os.cpu_count(), 1024) and cb["kind"] == "port" and cb["value"] > 0
-    assert ("per_gpu_share" in cb) == (os.cpu_count() > 16)
+    assert cb["cores"] == th["threads"] and cb["kind"] == "port" and cb["value"] > 0
+    assert ("per_gpu_share" in cb) == (th["threads"] > 16)
 
 
 def test_rccl_rehearsal_flag_and_environment():

@@ -205,3 +205,78 @@ def test_settle_phase_runs_the_same_frames_on_every_rank(tmp_path):
         assert p.exitcode == 0
     counts = [[x[1] for x in json.load(open(tmp_path / f"rank{r}.log")) if x[0] == "frames"][0] for r in range(world)]
     assert len(set(counts)) == 1 and counts[0] > 2 + 3, counts
+
+
+# ---- plain `python bench.py --gpus N` (no launcher): bench.py spawns the rank processes itself ----
+def test_launch_plan_picks_the_spawner_for_plain_multi_gpu_runs():
+    import bench
+    p = lambda argv, env=None: bench.launch_plan(bench.parse_args(argv), env or {})  # noqa: E731
+    assert p([]) == "group" and p(["--gpus", "1"]) == "group"
+    assert p(["--gpus", "8"]) == "spawn" and p(["--gpus", "2", "--rccl-rehearsal"]) == "spawn"
+    assert p(["--gpus", "8", "--one-process"]) == "group"                      # explicit, labelled "unrehearsed"
+    assert p(["--gpus", "3", "--transport", "copy", "--devices", "0,0,0"]) == "group"
+    assert p(["--gpus", "4", "--transport", "direct"]) == "group"
+    assert p(["--gpus", "4"], {"WORLD_SIZE": "4"}) == "ranks"                   # under torchrun: this is one rank
+
+
+def test_main_spawns_before_touching_the_gpu(monkeypatch):
+    """main() hands a plain N-GPU run to spawn_ranks before importing wcpt (no HIP call, no device query in the
+    parent), with the argv unchanged, and returns the ranks' status."""
+    import bench
+    seen = {}
+
+    def fake_spawn(argv, n, **kw):
+        seen.update(argv=list(argv), n=n, wcpt_loaded=bench.wcpt is not None)
+        return 5
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "wcpt", None)
+    monkeypatch.setattr(bench, "spawn_ranks", fake_spawn)
+    argv = ["--gpus", "4", "--config", "c1", "--steps", "3"]
+    assert bench.main(argv) == 5
+    assert seen == {"argv": argv, "n": 4, "wcpt_loaded": False}
+
+
+def _spawn(tmp_path, world, extra_env=None, argv=None):
+    import bench
+    env = dict(os.environ, WCPT_TEST_OUT=str(tmp_path), **(extra_env or {}))
+    env.pop("WORLD_SIZE", None)
+    argv = argv or ["--gpus", str(world), "--config", "c1", "--steps", "3", "--warmup", "2", "--settle-ms", "0",
+                    "--no-cpu-baseline"]
+    child = [sys.executable, os.path.join(ROOT, "tests", "bench_spawn_child.py")]
+    t0 = time.monotonic()
+    rc = bench.spawn_ranks(argv, world, env=env, child_cmd=child, timeout_s=240)
+    return rc, time.monotonic() - t0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_spawned_ranks_run_the_one_process_per_gpu_path(tmp_path, capfd, world):
+    rc, _ = _spawn(tmp_path, world)
+    out = capfd.readouterr().out
+    assert rc == 0
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1                                   # one JSON line, rank 0's, on the spawner's stdout
+    d = json.loads(lines[0])
+    assert d["ranks"] == world and d["n_gpus"] == world
+    assert d["launch"].startswith("spawned by bench.py")
+    assert d["group"]["kind"].startswith("one process per GPU") and d["group"]["transport"] == "rccl"
+    runs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    ids = {r["env"]["TORCHELASTIC_RUN_ID"] for r in runs}
+    ports = {r["env"]["MASTER_PORT"] for r in runs}
+    assert len(ids) == 1 and len(ports) == 1                 # one job: one rendezvous token and port for all ranks
+    for r, run in enumerate(runs):
+        e = run["env"]
+        assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"], e["LOCAL_WORLD_SIZE"]) == (str(r), str(r), str(world),
+                                                                                        str(world))
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["WCPT_BENCH_LAUNCH"] == "spawn"
+        assert ["group", r, world, r] in run["log"] and ["closed"] in run["log"]
+        assert not run["torch"]
+
+
+def test_a_failing_rank_stops_the_others(tmp_path, capfd):
+    """Rank 1 exits 7 before the rendezvous; the others would wait for it (up to the rendezvous timeout). The spawner
+    stops them at once and returns rank 1's status."""
+    rc, dt = _spawn(tmp_path, 3, extra_env={"WCPT_TEST_FAIL_RANK": "1"})
+    err = capfd.readouterr().err
+    assert rc == 7 and dt < 60
+    assert "rank 1 exited with 7" in err

@@ -217,3 +217,61 @@ def test_direct_transport_plans_only_renders(shim, overlap):
     n = 8
     steps = plan(shim, n, 0, overlap, 2, list(range(n)), [True, False, True])
     assert [(s["frame"], s["op"], s["rank"]) for s in steps] == [(f, RENDER, r) for f in range(3) for r in range(n)]
+
+
+# ---- the bounded wait of wcpt_group_sync (csrc/group_wait.h) ------------------------------------------------------------
+DONE, FAILED, TRANSPORT_ERROR, TIMED_OUT = range(4)
+
+
+def wait(shim, ready_after=-1, error_after=-1, fail_at=-1, timeout_ms=1000.0, ms_per_poll=0.001):
+    f = shim.wait_sim
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    f.restype = ctypes.c_int
+    el, polls, naps = ctypes.c_double(), ctypes.c_int(), ctypes.c_int()
+    r = f(ready_after, error_after, fail_at, timeout_ms, ms_per_poll, ctypes.byref(el), ctypes.byref(polls),
+          ctypes.byref(naps))
+    return r, el.value, polls.value, naps.value
+
+
+def test_bounded_wait_returns_when_the_streams_drain(shim):
+    r, el, polls, naps = wait(shim, ready_after=3)
+    assert (r, polls, naps) == (DONE, 4, 0)            # a stream that drains at once: spins, never sleeps
+    r, el, polls, naps = wait(shim, ready_after=5000, timeout_ms=60000.0)  # a long frame: naps of up to 1 ms
+    assert r == DONE and polls == 5001 and 0 < naps < polls and el <= 5001 * 1.001
+
+
+def test_peer_that_never_posts_ends_in_a_timeout(shim):
+    """a rank whose peer died (or skipped its part of a frame) has a transfer that never completes.
+    The sync's wait ends at the group's timeout (the caller then aborts the communicators and returns
+    WCPT_ERROR_DEVICE_LOST) instead of blocking for ever; the naps are bounded, so it ends within a nap of it."""
+    for timeout in (50.0, 3000.0):
+        r, el, polls, naps = wait(shim, ready_after=-1, timeout_ms=timeout)
+        assert r == TIMED_OUT
+        assert timeout <= el <= timeout + 1.0 + 0.002
+        assert polls < timeout * 10                    # it sleeps between polls: no busy spin for the whole wait
+
+
+def test_transport_error_ends_the_wait_before_the_timeout(shim):
+    r, el, polls, naps = wait(shim, ready_after=-1, error_after=40, timeout_ms=60000.0)
+    assert r == TRANSPORT_ERROR and polls == 41 and el < 60000.0
+
+
+def test_failed_poll_and_no_deadline(shim):
+    assert wait(shim, ready_after=-1, fail_at=7)[0] == FAILED
+    # timeout 0 (WCPT_GROUP_OPTION_TIMEOUT_MS = 0): no deadline; only a drain, an error or a failed poll ends it
+    r, el, polls, naps = wait(shim, ready_after=20000, timeout_ms=0.0)
+    assert r == DONE and el > 1000.0
+
+
+def test_a_skipped_frame_leaves_the_root_one_receive_without_a_send(shim):
+    """RCCL pairs a rank's sends with the root's receives in posting order. A rank that skips one frame's
+    wcpt_group_render posts one send fewer than the root posts receives, so the root's last receive -- and everything
+    queued behind it on its communication stream -- never completes: exactly the wait the bound above ends."""
+    n, root, frames, skip = 2, 0, 5, 3
+    per = [plan(shim, n, root, True, False, [r], [True] * (frames if r == root else frames - 1)) for r in range(n)]
+    recvs = [s for s in per[root] if s["op"] == RECV and s["peer"] == 1]
+    sends = [s for s in per[1] if s["op"] == SEND]
+    assert len(recvs) == frames and len(sends) == frames - 1
+    assert skip < frames and recvs[-1]["stream"] == COMM_STREAM
+    assert wait(shim, ready_after=-1, timeout_ms=100.0)[0] == TIMED_OUT

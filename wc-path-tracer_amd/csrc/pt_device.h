@@ -1039,9 +1039,11 @@ struct LdsStack {
             e = base[sp * 64];
         } else {
             e = spill[sp - N];
-#if WCPT_STACK_SPILL_WAIT
+#if WCPT_STACK_SPILL_WAIT && defined(__gfx9__)
             /* wait for the spill load inside its (rare) branch: otherwise the LDS read of the other lanes, which
-             * writes the same registers, waits for vmcnt(0) on every pop -- and so for every store still in flight */
+             * writes the same registers, waits for vmcnt(0) on every pop -- and so for every store still in flight.
+             * The immediate is the gfx9 s_waitcnt encoding (gfx950 is gfx9); other generations lay the counters out
+             * differently and get no explicit wait. */
             __builtin_amdgcn_s_waitcnt(0x0F70); /* vmcnt(0), expcnt/lgkmcnt untouched (gfx9 encoding) */
 #endif
         }

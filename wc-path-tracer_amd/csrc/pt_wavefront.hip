@@ -594,7 +594,10 @@ void wf_trace(const wcpt_scene_data sd, const wcpt_draw_command* __restrict__ dr
                         ray = ps.ray;
                         rt = rt0;
                         prim = prim0;
-                        any = WCPT_LAST_SEGMENT_SHORTCUT && ps.bounce + 1u > sd.maxBounceCount && sample + 1u == sd.samples;
+                        /* the queue-fetch path's guard (:392): any-hit only where that build option is on, and never
+                         * in a counting pass (which walks the reference's full closest-hit traversal) */
+                        any = !COUNT && WCPT_WF_ANYHIT_LAST && WCPT_LAST_SEGMENT_SHORTCUT &&
+                              ps.bounce + 1u > sd.maxBounceCount && sample + 1u == sd.samples;
                         d = 0;
                         start_draw();
                     } else {

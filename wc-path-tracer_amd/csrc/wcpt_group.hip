@@ -46,6 +46,7 @@
 
 #include "../../include/wcpt.h"
 #include "group_plan.h"
+#include "group_wait.h"
 #include "pt_kernels.h"
 
 static_assert(sizeof(ncclUniqueId) == WCPT_GROUP_UNIQUE_ID_BYTES, "WCPT_GROUP_UNIQUE_ID_BYTES");
@@ -54,6 +55,10 @@ namespace {
 
 constexpr int kPayloadBuffers = wcpt::plan::kPayloadBuffers;
 namespace plan = wcpt::plan;
+namespace gwait = wcpt::gwait;
+/* The default bound on one wcpt_group_sync of a group of several ranks. An editor loop syncs every frame (main.jai:73-95);
+ * bench.py syncs after at most a few hundred frames (c4 at 8 ranks: ~45 ms each). */
+constexpr int kDefaultTimeoutMs = 60000;
 
 /* One rank driven by this process. */
 struct LocalRank {
@@ -122,9 +127,12 @@ struct wcpt_group {
     uint64_t frames = 0;
     std::vector<wcpt::plan::RankState> plan_state; /* scratch of wcpt_group_render (no per-frame allocation) */
     std::vector<wcpt::plan::Step> steps;
-    /* WCPT_GROUP_OPTION_THREADS: -1 (default) on when this process's ranks span more than one device (COPY, DIRECT),
-     * 0 off, 1 on */
-    int threads = -1;
+    /* WCPT_GROUP_OPTION_THREADS: 0 (default) off, 1 on, -1 on when this process's ranks span more than one device
+     * (COPY, DIRECT). Off by default: the threaded issue has run only with every rank on one device. */
+    int threads = 0;
+    /* WCPT_GROUP_OPTION_TIMEOUT_MS: -1 (default) = kDefaultTimeoutMs in a group of several ranks, none in a group of
+     * one; 0 = wait forever */
+    int timeout_ms = -1;
     std::vector<std::unique_ptr<Worker>> workers; /* local ranks 1..n-1 (the caller's thread issues local rank 0) */
     std::atomic<bool> stopping{false};
     std::atomic<uint32_t> done{0};
@@ -541,6 +549,81 @@ int issue_frame(wcpt_group* g, const wcpt_scene_data* scene, const uint64_t* mat
     return WCPT_SUCCESS;
 }
 
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+double timeout_of(const wcpt_group* g)
+{
+    if (g->timeout_ms >= 0) return (double)g->timeout_ms;
+    return g->nranks > 1 ? (double)kDefaultTimeoutMs : 0.0;
+}
+
+/* Wait, bounded (group_wait.h), until local rank lr's render stream and communication stream have drained. Returns
+ * WCPT_SUCCESS; a failed poll (hip_fail); or, on an RCCL asynchronous error or the deadline t0 + the group's timeout,
+ * WCPT_ERROR_DEVICE_LOST with the communicators aborted (break_group): the frame's exchange cannot complete, since a
+ * peer failed or did not post its part. */
+int wait_rank(wcpt_group* g, LocalRank& lr, double t0)
+{
+    const hipStream_t streams[2] = {wcpt::context_stream(lr.ctx), lr.comm_stream};
+    const char* names[2] = {"render", "communication"};
+    for (int k = 0; k < 2; k++) {
+        if (!streams[k]) continue;
+        if (hipSetDevice(lr.device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+        hipError_t failed = hipSuccess;
+        ncclResult_t async = ncclSuccess;
+        const gwait::Result r = gwait::wait_for(
+            [&]() {
+                const hipError_t e = hipStreamQuery(streams[k]);
+                if (e == hipSuccess) return (int)gwait::kReady;
+                if (e == hipErrorNotReady) return (int)gwait::kBusy;
+                failed = e;
+                return (int)gwait::kPollError;
+            },
+            [&]() {
+                if (!lr.comm) return false;
+                ncclResult_t a = ncclSuccess;
+                if (ncclCommGetAsyncError(lr.comm, &a) != ncclSuccess) return false;
+                if (a == ncclSuccess || a == ncclInProgress) return false;
+                async = a;
+                return true;
+            },
+            t0, timeout_of(g), now_ms,
+            [](double us) { std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(us)); });
+        switch (r) {
+        case gwait::kDone:
+            break;
+        case gwait::kFailed:
+            (void)hipGetLastError();
+            return hip_fail(failed, names[k][0] == 'r' ? "hipStreamQuery(render)" : "hipStreamQuery(communication)");
+        case gwait::kTransportError:
+            return break_group(g, group_error(WCPT_ERROR_DEVICE_LOST, "rank %d: RCCL asynchronous error on the %s "
+                                              "stream: %s (communicators aborted)", lr.rank, names[k],
+                                              ncclGetErrorString(async)));
+        case gwait::kTimedOut:
+            return break_group(g, group_error(WCPT_ERROR_DEVICE_LOST, "rank %d: the %s stream did not drain within "
+                                              "%.0f ms (WCPT_GROUP_OPTION_TIMEOUT_MS): a peer failed or did not post "
+                                              "its part of a frame's exchange (communicators aborted)", lr.rank,
+                                              names[k], timeout_of(g)));
+        }
+    }
+    return WCPT_SUCCESS;
+}
+
+/* After the communicators were aborted: give the streams a bounded time to drain (RCCL's aborted kernels exit), so
+ * that destroying the group does not block on them. */
+void drain_after_abort(wcpt_group* g)
+{
+    const double t0 = now_ms();
+    const int saved = g->timeout_ms;
+    const double bound = timeout_of(g);
+    g->timeout_ms = bound > 0.0 && bound < 10000.0 ? (int)bound : 10000;
+    for (LocalRank& lr : g->local) (void)wait_rank(g, lr, t0);
+    g->timeout_ms = saved;
+    (void)hipGetLastError();
+}
+
 } // namespace
 
 extern "C" {
@@ -690,6 +773,15 @@ int wcpt_group_destroy(wcpt_group* g)
         g_timers = StepTimers();
     }
 #endif
+    {
+        /* bounded, as in wcpt_group_sync: a peer that died leaves this process's transfers unmatched; abort them
+         * (ncclCommAbort) rather than block here, then let the aborted work drain */
+        const double t0 = now_ms();
+        bool ok = true;
+        for (LocalRank& lr : g->local)
+            if (lr.ctx && wait_rank(g, lr, t0) != WCPT_SUCCESS) ok = false;
+        if (!ok || g->broken) drain_after_abort(g);
+    }
     for (LocalRank& lr : g->local) {
         if (lr.ctx) (void)wcpt_sync(lr.ctx);
         if (lr.comm_stream) {
@@ -739,6 +831,11 @@ int wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uin
 int wcpt_group_set_option(wcpt_group* g, int option, int value)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    if (option == WCPT_GROUP_OPTION_TIMEOUT_MS) {
+        if (value < 0) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group timeout %d ms (>= 0; 0 = none)", value);
+        g->timeout_ms = value;
+        return WCPT_SUCCESS;
+    }
     if (option == WCPT_GROUP_OPTION_THREADS) {
         if (value < -1 || value > 1) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group threads %d (-1, 0, 1)", value);
         g->threads = value;
@@ -863,6 +960,21 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
     if (!g->width) return group_error(WCPT_ERROR_NO_SCREEN, "wcpt_group_render: no screen (wcpt_group_create_screen)");
     const size_t nl = g->local.size();
     const bool exchange = presenting(g) && g->nranks > 1;
+    /* 0. the senders' payload buffers (attach_payloads sized them; a failed attach leaves one missing): a refusal
+     * before any device work, so a one-process group stays usable (split_refusal), instead of the plan's
+     * set-output step failing after other ranks' steps were issued */
+    if (exchange && g->transport != WCPT_GROUP_TRANSPORT_DIRECT) {
+        for (const LocalRank& lr : g->local) {
+            if (lr.rank == g->root) continue;
+            uint32_t y0 = 0, rows = 0;
+            block_of(g, lr.rank, y0, rows);
+            const uint64_t bytes = (uint64_t)g->width * rows * pixel_bytes(g->format);
+            for (int b = 0; b < kPayloadBuffers; b++)
+                if (!lr.payload[b] || lr.payload_cap[b] < bytes)
+                    return split_refusal(g, group_error(WCPT_ERROR_INVALID_ARGUMENT, "rank %d: payload missing (set "
+                                                        "the output again)", lr.rank));
+        }
+    }
     /* 1. every rank's arguments first: an argument error leaves every accumulation image as it was. In a group whose
      * other ranks live in other processes, those processes still post their part of this frame's exchange; this one
      * cannot, so its communicator is aborted (the exchange fails there instead of waiting for a send that never
@@ -891,22 +1003,23 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
 int wcpt_group_sync(wcpt_group* g)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    /* bounded: poll every local rank's streams (group_wait.h) instead of blocking in hipStreamSynchronize, so a peer
+     * that failed or skipped a frame ends in WCPT_ERROR_DEVICE_LOST after the group's timeout, not in a hang */
+    const double t0 = now_ms();
     int first = WCPT_SUCCESS;
     for (LocalRank& lr : g->local) {
-        int rc = wcpt_sync(lr.ctx);
-        if (!rc && lr.comm_stream) {
-            (void)hipSetDevice(lr.device);
-            const hipError_t e = hipStreamSynchronize(lr.comm_stream);
-            if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize(communication)");
-        }
+        int rc = wait_rank(g, lr, t0);
+        if (!rc) rc = wcpt_sync(lr.ctx); /* drained: returns at once, with the render status (stack overflow) */
         if (!rc) free_retired(lr);
         if (!rc && lr.comm) {
             ncclResult_t async = ncclSuccess;
-            if (ncclCommGetAsyncError(lr.comm, &async) == ncclSuccess && async != ncclSuccess)
+            if (ncclCommGetAsyncError(lr.comm, &async) == ncclSuccess && async != ncclSuccess &&
+                async != ncclInProgress)
                 rc = break_group(g, nccl_fail(async, "RCCL asynchronous error"));
         }
         if (rc && !first) first = rc;
     }
+    if (first && g->broken) drain_after_abort(g);
     if (!first && g->broken) first = group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
     return first;
 }

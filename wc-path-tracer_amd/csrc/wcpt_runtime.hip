@@ -830,8 +830,8 @@ int wcpt_set_kernel(wcpt_context* ctx, int variant)
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
     if (variant != WCPT_KERNEL_MEGAKERNEL && variant != WCPT_KERNEL_WAVEFRONT && variant != WCPT_KERNEL_AUTO)
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", variant);
+    if (ctx->kernel != variant) ctx->generation++; /* the cached frame preparation resolved the variant */
     ctx->kernel = variant;
-    ctx->generation++; /* the cached frame preparation resolved the variant */
     return WCPT_SUCCESS;
 }
 
@@ -846,7 +846,9 @@ int wcpt_last_kernel(wcpt_context* ctx, int* variant)
 int wcpt_set_option(wcpt_context* ctx, int option, int value)
 {
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
-    ctx->generation++; /* options decide the cached frame preparation (record formats, layouts, the cache itself) */
+    /* The options that prepare_tri_records / render_validate read (record formats, stack-entry layout, the cache
+     * itself) invalidate their cached frame preparation once accepted: ctx->generation++ there only, so a host that
+     * sets the other options every frame keeps the cache. */
     switch (option) {
     case WCPT_OPTION_SORT_RAYS:
         ctx->sort_rays = value ? 1 : 0;
@@ -865,13 +867,16 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         return WCPT_SUCCESS;
     case WCPT_OPTION_PACKED_REFS:
         ctx->packed_refs = value ? 1 : 0;
+        ctx->generation++;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PAIR_RECORDS:
         if (value < -1 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pair records %d", value);
         ctx->pair_records = value;
+        ctx->generation++;
         return WCPT_SUCCESS;
     case WCPT_OPTION_TRIANGLE_CACHE:
         ctx->tri_cache = value ? 1 : 0;
+        ctx->generation++;
         return WCPT_SUCCESS;
     case WCPT_OPTION_WF_STACK:
         if (value != 10 && value != 16 && value != 24)

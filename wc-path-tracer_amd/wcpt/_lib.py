@@ -91,6 +91,7 @@ GROUP_TRANSPORT_DIRECT = 2
 GROUP_UNIQUE_ID_BYTES = 128
 GROUP_OPTION_OVERLAP = 1
 GROUP_OPTION_THREADS = 2
+GROUP_OPTION_TIMEOUT_MS = 3
 ABI_VERSION = 4
 assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
 assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
