@@ -430,6 +430,9 @@ def parse_args(argv=None):
                     help="N > 1 without a launcher: drive every rank from this one process and thread "
                          "(wcpt_group_create_ex; RCCL ncclCommInitAll) instead of spawning one process per GPU. With "
                          "RCCL over several GPUs this form has never run on hardware, and the line says so")
+    ap.add_argument("--row-stripe", type=int, default=0,
+                    help="N > 1: interleaved row stripes of this many rows (WCPT_GROUP_OPTION_ROW_STRIPE; rank r renders "
+                         "stripes r, r + N, ...) instead of contiguous row blocks (0, the default)")
     ap.add_argument("--group-timeout-ms", type=int, default=None,
                     help="WCPT_GROUP_OPTION_TIMEOUT_MS: how long wcpt_group_sync waits for a frame's exchange before "
                          "it aborts the communicator and returns WCPT_ERROR_DEVICE_LOST (default: the library's; "
@@ -527,6 +530,8 @@ def resolve_topology(args, env) -> dict:
         local = int(env.get("LOCAL_RANK", env.get("RANK", "0")))
         if args.rccl_rehearsal and args.dist_backend != "rccl":
             raise SystemExit("bench.py: --rccl-rehearsal rehearses the RCCL group (--dist-backend rccl)")
+        if args.row_stripe and args.dist_backend != "rccl":
+            raise SystemExit("bench.py: --row-stripe is an option of the C-ABI group (--dist-backend rccl)")
         return {"mode": "ranks" if args.dist_backend == "rccl" else "torch", "nranks": world,
                 "rank": int(env.get("RANK", "0")), "local_rank": local, "devices": [local]}
     if args.dist_backend != "rccl":
@@ -626,6 +631,8 @@ class GroupBench:
             self.g.set_option(T.GROUP_OPTION_THREADS, args.group_threads)
         if getattr(args, "group_timeout_ms", None) is not None:
             self.g.set_option(T.GROUP_OPTION_TIMEOUT_MS, args.group_timeout_ms)
+        if getattr(args, "row_stripe", 0):
+            self.g.set_option(T.GROUP_OPTION_ROW_STRIPE, args.row_stripe)
         self.g.create_screen(W, H)
         self.fmt, self.px = GATHER_FORMATS[args.gather]
         self.out = None
@@ -1075,7 +1082,8 @@ def main(argv=None):
                        "camera": args.camera,
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel] +
                                  (" (WCPT_KERNEL_AUTO's choice)" if args.kernel_auto else ""), "bvh": args.bvh,
-                       "parallelism": (f"row-block x{nranks} + {transport} gather of {args.gather} blocks"
+                       "parallelism": ((f"row-stripes of {args.row_stripe} rows x{nranks}" if args.row_stripe else
+                                        f"row-block x{nranks}") + f" + {transport} gather of {args.gather} blocks"
                                        + ("" if args.no_overlap else " overlapped with the next frame")
                                        if nranks > 1 else "one device")},
             "ranks": nranks,

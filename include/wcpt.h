@@ -125,6 +125,11 @@ extern "C" {
  * another and shades between them, for one sample per pixel on one-draw scenes. -1 (default): where the frame has at
  * most 1.4 paths per resident lane of it (row blocks), 0 never, 1 whenever eligible. Same results. */
 #define WCPT_OPTION_WF_PERSIST 13
+/* The gather output (wcpt_set_gather_output) addressed by frame row: 1 = the pixel of frame row y goes to row y of
+ * the output (a buffer of the whole frame, which several contexts can share, each writing only its own rows -- rows
+ * blocks or interleaved stripes alike); 0 (default) = the context's rows back to back (row ly of its rows at row ly).
+ * Added under ABI 4. */
+#define WCPT_OPTION_GATHER_FRAME_ROWS 14
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 
@@ -285,6 +290,14 @@ int      wcpt_resize(wcpt_context* ctx, uint32_t width, uint32_t height);
 /* Row-block shard: this context renders and stores only rows [y0, y0+rows) of the width x height
  * frame (global pixel indices and seeds unchanged). rows == 0 resets to the full frame. */
 int      wcpt_set_row_range(wcpt_context* ctx, uint32_t y0, uint32_t rows);
+/* Interleaved row stripes (SURVEY.md §8(e)'s fallback when static blocks cap the scaling): this context renders
+ * `rows` rows of the frame -- stripes of `stripe` rows every `period` rows, the first starting at frame row y_first,
+ * the last possibly short -- and stores them back to back ([rows][width]): local row ly is frame row
+ * y_first + ly + (ly / stripe) * (period - stripe). Seeds and pixel indices stay global (pathTracer.comp:304), so the
+ * rows are bit-identical to a whole-frame render's. `stripe` is a power of two (1..32768), period >= stripe;
+ * stripe == 0 is wcpt_set_row_range(y_first, rows). wcpt_row_stripes gives rank r of n its (y_first, rows) for
+ * period = n * stripe. Added under ABI 4. */
+int      wcpt_set_row_stripes(wcpt_context* ctx, uint32_t y_first, uint32_t rows, uint32_t stripe, uint32_t period);
 uint64_t wcpt_image_device_ptr(wcpt_context* ctx);                 /* float4[rows][width], pitch width*16 */
 /* Render into caller-owned device memory (e.g. a torch tensor handed to RCCL, or imported interop memory)
  * instead of the context's own image. `bytes` must hold width*rows*16. device_ptr == 0 reverts to the
@@ -391,6 +404,11 @@ int      wcpt_read_diagnostics(wcpt_context* ctx, uint64_t* out, uint32_t n);
 /* The row-block split itself, for a host that runs one process per device (then wcpt_set_row_range with the
  * result): rank r of n renders rows [r*height/n, (r+1)*height/n). Host-only, no device needed. */
 int           wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uint32_t* rows);
+/* The interleaved split (wcpt_set_row_stripes with period = n * stripe): rank r of n takes the stripes r, r + n,
+ * r + 2n, ... of `stripe` rows; *y_first = r * stripe, *rows = the rows it holds (0 when the frame has fewer than r + 1
+ * stripes). stripe == 0 is wcpt_row_block. Host-only. Added under ABI 4. */
+int           wcpt_row_stripes(uint32_t height, uint32_t n, uint32_t rank, uint32_t stripe, uint32_t* y_first,
+                               uint32_t* rows);
 typedef struct wcpt_group wcpt_group;
 #define WCPT_GROUP_TRANSPORT_RCCL 0
 #define WCPT_GROUP_TRANSPORT_COPY 1
@@ -419,6 +437,15 @@ typedef struct wcpt_group wcpt_group;
  * WCPT_ERROR_DEVICE_LOST). Pick it above the longest run of frames the host queues between two syncs. Option 3 was
  * added under ABI 4. */
 #define WCPT_GROUP_OPTION_TIMEOUT_MS 3
+/* Rows per interleaved stripe of the group's split: 0 (default) = contiguous row blocks (wcpt_row_block); a power of
+ * two = rank r renders the stripes r, r + n, r + 2n, ... of that many rows (wcpt_row_stripes), so every rank gets rows
+ * from the whole frame and a scene whose cost sits in one region no longer loads one rank. Multiples of 8 keep the
+ * kernels' 8x8 tiles inside a stripe. The presented frame is the same bits either way: the root renders its stripes
+ * straight into their rows of the output, RCCL blocks arrive in a root-side staging buffer and are copied to their rows
+ * on the root's communication stream (hipMemcpy2DAsync), COPY senders copy their stripes to their rows, and DIRECT
+ * senders write their rows themselves. Every process sets the same value; takes effect at once (the screen is laid
+ * out again and accumulation restarts). Added under ABI 4. */
+#define WCPT_GROUP_OPTION_ROW_STRIPE 4
 typedef struct wcpt_group_info {
     int32_t nranks;            /* ranks of the group; RCCL: ncclCommCount of this process's first communicator */
     int32_t local_ranks;       /* ranks driven by this process */

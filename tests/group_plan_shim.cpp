@@ -6,7 +6,7 @@
 #include "../wc-path-tracer_amd/csrc/group_plan.h"
 
 extern "C" int plan_frames(int nranks, int root, int overlap, int transport, int nlocal, const int32_t* local_ranks,
-                           const int32_t* presenting, int frames, int32_t* out, int cap)
+                           const int32_t* presenting, int frames, int32_t* out, int cap, int stripes)
 {
     std::vector<wcpt::plan::RankState> local(nlocal);
     for (int i = 0; i < nlocal; i++) local[i] = {local_ranks[i], {false, false}};
@@ -14,7 +14,7 @@ extern "C" int plan_frames(int nranks, int root, int overlap, int transport, int
     int n = 0;
     for (int f = 0; f < frames; f++) {
         const bool exchange = presenting[f] != 0 && nranks > 1;
-        wcpt::plan::frame_steps(nranks, root, overlap != 0, exchange, transport, (uint64_t)f, local, steps);
+        wcpt::plan::frame_steps(nranks, root, overlap != 0, exchange, transport, (uint64_t)f, local, steps, stripes != 0);
         for (const wcpt::plan::Step& s : steps) {
             if (n >= cap) return -1;
             int32_t* o = out + 6 * n++;

@@ -29,6 +29,35 @@ def test_row_block_partition():
         row_block(10, 2, 2)
 
 
+def test_row_stripes_partition_the_frame():
+    """Interleaved row stripes (include/wcpt.h wcpt_row_stripes, its Python mirror and the row map
+    of row_map.h): for every height, rank count and stripe size the ranks' frame rows cover the frame exactly once, the
+    library's split equals the mirror's, and every rank's rows fit the map's closed form."""
+    import ctypes as C
+    from wcpt import _lib
+    from wcpt.dist import frame_rows, row_stripes
+    y0, rows = C.c_uint32(), C.c_uint32()
+    for H in (1, 7, 17, 45, 135, 1080, 1081, 2160):
+        for N in (1, 2, 3, 4, 7, 8):
+            for S in (0, 1, 2, 8, 16, 64):
+                stripes = -(-H // S) if S else H
+                if stripes < N:
+                    continue
+                seen = []
+                for r in range(N):
+                    assert _lib.lib.wcpt_row_stripes(H, N, r, S, C.byref(y0), C.byref(rows)) == 0
+                    assert (y0.value, rows.value) == row_stripes(H, N, r, S)
+                    fr = frame_rows(H, N, r, S)
+                    assert len(fr) == rows.value > 0 and fr == sorted(fr)
+                    seen += fr
+                assert sorted(seen) == list(range(H)), (H, N, S)
+    # 1080 rows, 8 ranks, stripes of 8: 135 stripes -> ranks 0-6 hold 17 (136 rows), rank 7 holds 16 (128 rows)
+    assert [row_stripes(1080, 8, r, 8)[1] for r in range(8)] == [136] * 7 + [128]
+    assert _lib.lib.wcpt_row_stripes(100, 2, 0, 3, C.byref(y0), C.byref(rows)) != 0   # not a power of two
+    with pytest.raises(ValueError):
+        row_stripes(100, 2, 0, 6)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

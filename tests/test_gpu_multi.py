@@ -28,13 +28,13 @@ pytestmark = pytest.mark.gpu
 PB = wcpt._lib.PAYLOAD_PIXEL_BYTES
 
 
-def _context_frames(s, W, H, frames, bounces=4, kernel=wcpt.KERNEL_MEGAKERNEL):
+def _context_frames(s, W, H, frames, bounces=4, kernel=wcpt.KERNEL_MEGAKERNEL, samples=1):
     with wcpt.Context(0) as ctx:
         dev = wcpt.DeviceScene(ctx, s)
         ctx.set_kernel(kernel)
         ctx.create_screen(W, H)
         for f in frames:
-            ctx.render(s.scene_data(W, H, max_bounce=bounces, frame=f), *dev.addresses())
+            ctx.render(s.scene_data(W, H, max_bounce=bounces, samples=samples, frame=f), *dev.addresses())
         ctx.sync()
         img = ctx.readback()
         dev.free()
@@ -236,10 +236,13 @@ def test_two_ranks_display_payload_gather_equals_oracle_composite(gpu_ctx, tmp_p
 COPY = wcpt._lib.GROUP_TRANSPORT_COPY
 
 
-def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, threads=-1, transport=COPY, root=0):
+def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, threads=-1, transport=COPY, root=0,
+                  stripe=0, samples=1):
     """Progressive frames through an n-rank COPY (or DIRECT) group on device 0: (presented frame bytes, each rank's
-    block)."""
+    block). stripe > 0: interleaved row stripes (WCPT_GROUP_OPTION_ROW_STRIPE)."""
     with wcpt.Group([0] * n, root=root, transport=transport) as g:
+        if stripe:
+            g.set_option(wcpt._lib.GROUP_OPTION_ROW_STRIPE, stripe)
         devs = []
         for r in range(n):
             c = g.context(r)
@@ -254,7 +257,7 @@ def _group_frames(s, W, H, frames, n, fmt, kernel, overlap=True, bounces=4, thre
         g.set_output(fmt, rc.buffer_address(out), nbytes)
         addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
         for f in frames:
-            g.render(s.scene_data(W, H, max_bounce=bounces, frame=f), *addr)
+            g.render(s.scene_data(W, H, max_bounce=bounces, samples=samples, frame=f), *addr)
         g.sync()
         info = g.info()
         raw = rc.buffer_download(out, nbytes)
@@ -616,3 +619,118 @@ def test_device_pci_bus_id_names_the_gpu(gpu_ctx):
     assert re.fullmatch(r"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]", ident), ident
     with pytest.raises(wcpt.WcptError):
         wcpt.device_pci_bus_id(wcpt.device_count() + 7)
+
+
+# ---- interleaved row stripes (SURVEY.md §8(e)'s fallback; WCPT_GROUP_OPTION_ROW_STRIPE, wcpt_set_row_stripes) ----------
+@pytest.mark.parametrize("n,stripe", [(2, 8), (3, 8), (2, 16), (4, 8), (3, 1)])
+@pytest.mark.parametrize("transport", [COPY, DIRECT])
+@pytest.mark.parametrize("fmt", [wcpt._lib.PAYLOAD_RGB32F, wcpt._lib.PAYLOAD_DISPLAY_RGBA8])
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_group_row_stripes_equal_one_device(gpu_ctx, n, stripe, transport, fmt, kernel):
+    """Rank r renders the stripes r, r + n, ... (45 rows: the last stripe is short, and the ranks hold different row
+    counts); the root renders its stripes straight into their frame rows, COPY senders copy theirs to their rows
+    (hipMemcpy2DAsync), DIRECT senders write their rows themselves. Frame after frame the presented frame equals one
+    device's bit for bit, and each rank's accumulation holds exactly its frame rows."""
+    from wcpt.dist import frame_rows
+    s = get_scene("cornell")
+    W, H, frames = 72, 45, (0, 1, 2)
+    ref = _context_frames(s, W, H, frames, kernel=kernel)
+    raw, blocks = _group_frames(s, W, H, frames, n, fmt, kernel, transport=transport, root=n - 1, stripe=stripe)
+    got = _as_frame(raw, fmt, W, H)
+    if fmt == wcpt._lib.PAYLOAD_DISPLAY_RGBA8:
+        assert np.array_equal(got, oracle.composite(ref)[1])
+    else:
+        assert np.array_equal(got.view(np.uint32), ref[..., :3].view(np.uint32))
+    seen = []
+    for r, blk in enumerate(blocks):
+        rows = frame_rows(H, n, r, stripe)
+        seen += rows
+        assert np.array_equal(blk.view(np.uint32), ref[rows].view(np.uint32))
+    assert sorted(seen) == list(range(H))
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_group_row_stripes_in_line_multi_sample_and_relayout(gpu_ctx, kernel):
+    """Stripes with the gather in line (overlap off) and two samples per pixel (the wavefront shade recomputes the
+    primary ray of sample 1 from the frame row), then the option switched on an existing screen (the frame is laid out
+    again) -- every presented frame equals one device's."""
+    s = get_scene("default_dielectric")
+    W, H, frames = 48, 40, (0, 1, 2)
+    fmt = wcpt._lib.PAYLOAD_RGBA32F
+    ref = _context_frames(s, W, H, frames, kernel=kernel, bounces=3, samples=2)
+    raw, _ = _group_frames(s, W, H, frames, 3, fmt, kernel, overlap=False, bounces=3, stripe=8, samples=2)
+    assert np.array_equal(_as_frame(raw, fmt, W, H).view(np.uint32), ref.view(np.uint32))
+    ref1 = _context_frames(s, W, H, (0,), kernel=kernel, bounces=3)
+    with wcpt.Group([0] * 2, root=0, transport=COPY) as g:
+        devs = [wcpt.DeviceScene(g.context(r), s) for r in range(2)]
+        for r in range(2):
+            g.context(r).set_kernel(kernel)
+        g.create_screen(W, H)
+        out = g.context(0).buffer_alloc(W * H * 16)
+        g.set_output(fmt, g.context(0).buffer_address(out), W * H * 16)
+        addr = [list(a) for a in zip(*[d.addresses() for d in devs])]
+        g.render(s.scene_data(W, H, max_bounce=3, frame=0), *addr)
+        g.set_option(wcpt._lib.GROUP_OPTION_ROW_STRIPE, 16)          # re-laid out: blocks -> stripes
+        assert [c.height for c in g.contexts] == [24, 16]
+        g.render(s.scene_data(W, H, max_bounce=3, frame=0), *addr)
+        g.sync()
+        got = np.frombuffer(g.context(0).buffer_download(out, W * H * 16), np.float32).reshape(H, W, 4)
+        assert np.array_equal(got.view(np.uint32), ref1.view(np.uint32))
+        g.context(0).buffer_free(out)
+        for d in devs:
+            d.free()
+
+
+@pytest.mark.parametrize("kernel", [wcpt.KERNEL_MEGAKERNEL, wcpt.KERNEL_WAVEFRONT])
+def test_context_row_stripes_and_frame_row_output(gpu_ctx, kernel):
+    """wcpt_set_row_stripes on one context: its accumulation holds exactly the frame rows of the map, bit-identical to
+    a whole-frame render, and with WCPT_OPTION_GATHER_FRAME_ROWS its gather output writes them at their frame rows of a
+    shared whole-frame buffer (the other rows untouched)."""
+    s = get_scene("cornell")
+    W, H = 40, 52
+    ref = _context_frames(s, W, H, (0, 1), kernel=kernel)
+    for y_first, rows, stripe, period in ((3, 20, 4, 12), (0, 13, 8, 16), (5, 47, 1, 1), (8, 24, 8, 24)):
+        with wcpt.Context(0) as ctx:
+            dev = wcpt.DeviceScene(ctx, s)
+            ctx.set_kernel(kernel)
+            ctx.create_screen(W, H)
+            ctx.set_row_stripes(y_first, rows, stripe, period)
+            want = [y_first + ly + (ly // stripe) * (period - stripe) for ly in range(rows)]
+            nbytes = W * H * 16
+            out = ctx.buffer_from(np.full(nbytes // 4, -7.0, np.float32))
+            ctx.set_option(wcpt._lib.OPTION_GATHER_FRAME_ROWS, 1)
+            ctx.set_gather_output(ctx.buffer_address(out), nbytes, wcpt._lib.PAYLOAD_RGBA32F)
+            for f in (0, 1):
+                ctx.render(s.scene_data(W, H, max_bounce=4, frame=f), *dev.addresses())
+            ctx.sync()
+            blk = ctx.readback(rows)
+            wire = np.frombuffer(ctx.buffer_download(out, nbytes), np.float32).reshape(H, W, 4)
+            ctx.buffer_free(out)
+            dev.free()
+        assert np.array_equal(blk.view(np.uint32), ref[want].view(np.uint32)), (y_first, rows, stripe, period)
+        assert np.array_equal(wire[want].view(np.uint32), ref[want].view(np.uint32))
+        other = np.setdiff1d(np.arange(H), want)
+        assert (wire[other] == -7.0).all()
+
+
+def test_row_stripe_errors(gpu_ctx):
+    s = get_scene("cornell")
+    with wcpt.Context(0) as ctx:
+        ctx.create_screen(16, 20)
+        for args in ((0, 4, 3, 8), (0, 4, 8, 4), (0, 0, 8, 16), (8, 9, 8, 16)):   # not a power of two; period < stripe;
+            with pytest.raises(wcpt.WcptError):                               # no rows; past the frame (row 23)
+                ctx.set_row_stripes(*args)
+        ctx.set_row_stripes(4, 8, 4, 8)
+        ctx.create_screen(16, 12)        # rows 4..7 and 12..15: the new frame cannot hold them -> the whole frame again
+        assert ctx.readback().shape[0] == 12
+    with wcpt.Group([0] * 3, root=0, transport=COPY) as g:
+        for v in (-1, 3, 65536):
+            with pytest.raises(wcpt.WcptError):
+                g.set_option(wcpt._lib.GROUP_OPTION_ROW_STRIPE, v)
+        g.set_option(wcpt._lib.GROUP_OPTION_ROW_STRIPE, 8)
+        with pytest.raises(wcpt.WcptError):
+            g.create_screen(16, 16)      # two stripes of 8 rows for three ranks
+        g.create_screen(16, 17)          # three stripes: ranks hold 8, 8 and 1 rows
+        assert [c.height for c in g.contexts] == [8, 8, 1]
+        assert g.info()["broken"] == 0
+    del s

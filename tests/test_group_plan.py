@@ -24,7 +24,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "wc-path-tracer_amd", "csrc", "group_plan.h")
 
-WAIT_SENT, SET_OUTPUT, RENDER, RECORD_READY, COMM_WAIT_READY, SEND, RECV, RECORD_SENT = range(8)
+WAIT_SENT, SET_OUTPUT, RENDER, RECORD_READY, COMM_WAIT_READY, SEND, RECV, RECORD_SENT, SCATTER = range(9)
 RENDER_STREAM, COMM_STREAM = 0, 1
 
 
@@ -34,7 +34,7 @@ def _parse_header_ops():
     for line in open(HEADER):
         line = line.strip()
         for name in ("kWaitSent", "kSetOutput", "kRender", "kRecordReady", "kCommWaitReady", "kSend", "kRecv",
-                     "kRecordSent"):
+                     "kRecordSent", "kScatter"):
             if line.startswith(name + " ="):
                 ops[name] = int(line.split("=")[1].split(",")[0])
     return ops
@@ -47,17 +47,18 @@ def shim(tmp_path_factory):
     subprocess.run(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", src, "-o", str(out)], check=True)
     lib = ctypes.CDLL(str(out))
     I32P = ctypes.POINTER(ctypes.c_int32)
-    lib.plan_frames.argtypes = [ctypes.c_int] * 5 + [I32P, I32P, ctypes.c_int, I32P, ctypes.c_int]
+    lib.plan_frames.argtypes = [ctypes.c_int] * 5 + [I32P, I32P, ctypes.c_int, I32P, ctypes.c_int, ctypes.c_int]
     lib.plan_frames.restype = ctypes.c_int
     return lib
 
 
-def plan(shim, nranks, root, overlap, copy, local, presenting):
+def plan(shim, nranks, root, overlap, copy, local, presenting, stripes=False):
     cap = 100000
     out = (ctypes.c_int32 * (6 * cap))()
     loc = (ctypes.c_int32 * len(local))(*local)
     pres = (ctypes.c_int32 * len(presenting))(*[1 if p else 0 for p in presenting])
-    n = shim.plan_frames(nranks, root, int(overlap), int(copy), len(local), loc, pres, len(presenting), out, cap)
+    n = shim.plan_frames(nranks, root, int(overlap), int(copy), len(local), loc, pres, len(presenting), out, cap,
+                         int(stripes))
     assert n >= 0
     return [dict(frame=out[6 * i], op=out[6 * i + 1], rank=out[6 * i + 2], buffer=out[6 * i + 3],
                  peer=out[6 * i + 4], stream=out[6 * i + 5]) for i in range(n)]
@@ -154,7 +155,7 @@ def check_rules(ops, nranks, root, overlap, copy, presenting):
 def test_plan_orders_every_frame(shim, nranks, root, overlap, copy):
     assert _parse_header_ops() == dict(kWaitSent=WAIT_SENT, kSetOutput=SET_OUTPUT, kRender=RENDER,
                                        kRecordReady=RECORD_READY, kCommWaitReady=COMM_WAIT_READY, kSend=SEND,
-                                       kRecv=RECV, kRecordSent=RECORD_SENT)
+                                       kRecv=RECV, kRecordSent=RECORD_SENT, kScatter=SCATTER)
     presenting = [True, True, True, False, True, True, True, True, False, False, True, True]
     steps = plan(shim, nranks, root, overlap, copy, list(range(nranks)), presenting)
     for seed in range(6):
@@ -218,6 +219,42 @@ def test_direct_transport_plans_only_renders(shim, overlap):
     steps = plan(shim, n, 0, overlap, 2, list(range(n)), [True, False, True])
     assert [(s["frame"], s["op"], s["rank"]) for s in steps] == [(f, RENDER, r) for f in range(3) for r in range(n)]
 
+
+
+@pytest.mark.parametrize("nranks,root", [(2, 0), (4, 2), (8, 0)])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_row_stripes_scatter_each_received_block_after_its_transfer(shim, nranks, root, overlap):
+    """Interleaved row stripes over RCCL (WCPT_GROUP_OPTION_ROW_STRIPE): the root receives every block into its staging
+    buffer and then copies it to its frame rows (kScatter) on the same stream -- after the receive of that frame, before
+    the next frame's receive into the same staging area, and outside the ncclGroupStart/End (every send and receive of
+    the frame stay contiguous in the plan, so one host thread can post them in one group). COPY needs no scatter."""
+    presenting = [True, True, False, True, True, True]
+    steps = plan(shim, nranks, root, overlap, False, list(range(nranks)), presenting, stripes=True)
+    assert not [s for s in plan(shim, nranks, root, overlap, True, list(range(nranks)), presenting, stripes=True)
+                if s["op"] == SCATTER]
+    for f in range(len(presenting)):
+        fs = [s for s in steps if s["frame"] == f]
+        xfer = [i for i, s in enumerate(fs) if s["op"] in (SEND, RECV)]
+        assert xfer == list(range(xfer[0], xfer[-1] + 1)) if xfer else True      # one contiguous group
+        sc = [s for s in fs if s["op"] == SCATTER]
+        assert sorted(s["peer"] for s in sc) == ([r for r in range(nranks) if r != root] if presenting[f] else [])
+        for s in sc:
+            assert s["rank"] == root and fs.index(s) > xfer[-1]
+            assert s["stream"] == [r for r in fs if r["op"] == RECV and r["peer"] == s["peer"]][0]["stream"]
+    for seed in range(4):
+        rng = random.Random(seed)
+        ops = simulate([steps], lambda o: rng.uniform(1, 3) if o["op"] == RENDER else
+                       (rng.uniform(0.5, 5) if o["op"] in (SEND, RECV, SCATTER) else 0.0))
+        check_rules(ops, nranks, root, overlap, False, presenting)
+        recv_end = {(o["frame"], o["peer"]): o["end"] for o in ops if o["op"] == RECV}
+        recv_start = {(o["frame"], o["peer"]): o["start"] for o in ops if o["op"] == RECV}
+        for o in ops:
+            if o["op"] != SCATTER:
+                continue
+            assert o["start"] >= recv_end[(o["frame"], o["peer"])] - 1e-9
+            later = [t for (f, p), t in recv_start.items() if p == o["peer"] and f > o["frame"]]
+            if later:                                     # the next receive into this staging area waits for it
+                assert min(later) >= o["end"] - 1e-9
 
 # ---- the bounded wait of wcpt_group_sync (csrc/group_wait.h) ------------------------------------------------------------
 DONE, FAILED, TRANSPORT_ERROR, TIMED_OUT = range(4)

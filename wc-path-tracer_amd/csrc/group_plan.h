@@ -14,7 +14,10 @@
  *   4. the transfers: each sender sends payload b to the root and the root receives every other rank's block into its
  *      rows of the frame (RCCL: one ncclGroupStart/ncclGroupEnd around all of them), or each sender copies payload b
  *      into the root's frame (COPY transport: peer copies, no receive);
- *   5. sent[b] is recorded behind each sender's transfer.
+ *   5. interleaved row stripes (WCPT_GROUP_OPTION_ROW_STRIPE) with RCCL: the root received each block into a staging
+ *      buffer, and now copies each one's stripes to their rows of the frame on the same stream (after the whole
+ *      ncclGroupStart/End, so one host thread can post every rank's transfers of the frame in one group);
+ *   6. sent[b] is recorded behind each sender's transfer.
  * The buffer index alternates between frames with overlap on (b = frame % 2), so frame k + 1 renders while frame k's
  * transfer is in flight; with overlap off it is always 0, and the transfer is in line with the renders.
  * DIRECT transport: every sender's render writes its block straight into the root's frame over xGMI (its gather output
@@ -40,6 +43,7 @@ enum Op : int32_t {
     kSend = 5,          /* payload `buffer` to `peer` (the root): RCCL send, or a peer copy into the root's frame */
     kRecv = 6,          /* the root receives rank `peer`'s block into its frame (RCCL only)                     */
     kRecordSent = 7,    /* sent[buffer] recorded behind the rank's transfer                                     */
+    kScatter = 8,       /* the root copies rank `peer`'s received stripes from staging to their frame rows        */
 };
 
 enum Stream : int32_t { kRenderStream = 0, kCommStream = 1 };
@@ -62,7 +66,7 @@ inline int payload_buffer(bool overlap, uint64_t frame) { return overlap ? (int)
 /* The steps of frame `frame` for this process's ranks (`local`, in rank order), in issue order; marks sent[b] pending
  * for every sender whose transfer was planned. `exchange`: presenting with more than one rank. */
 inline void frame_steps(int nranks, int root, bool overlap, bool exchange, int transport, uint64_t frame,
-                        std::vector<RankState>& local, std::vector<Step>& out)
+                        std::vector<RankState>& local, std::vector<Step>& out, bool stripes = false)
 {
     out.clear();
     const bool copy = transport == kCopy;
@@ -92,6 +96,11 @@ inline void frame_steps(int nranks, int root, bool overlap, bool exchange, int t
         for (int r = 0; r < nranks; r++)
             if (r != root) out.push_back({kRecv, lr.rank, b, r, xs});
     }
+    if (stripes && !copy)
+        for (const RankState& lr : local)
+            if (lr.rank == root)
+                for (int r = 0; r < nranks; r++)
+                    if (r != root) out.push_back({kScatter, lr.rank, b, r, xs});
     for (RankState& lr : local) {
         if (lr.rank == root) continue;
         out.push_back({kRecordSent, lr.rank, b, -1, xs});

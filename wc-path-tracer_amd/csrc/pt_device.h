@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "../../include/wcpt.h"
+#include "row_map.h"
 #include "wcpt_composite.h"
 #include "wcpt_libm.h"
 
@@ -1791,20 +1792,27 @@ __device__ __noinline__ uint32_t display_rgba8(f3 acc)
     return (uint32_t)wcpt_unorm8(o[0]) | ((uint32_t)wcpt_unorm8(o[1]) << 8) | ((uint32_t)wcpt_unorm8(o[2]) << 16) |
            (255u << 24);
 }
+/* Gather-output rows (row_map.h): the map {0, 31, 0} (row = ly) addresses a payload that holds the context's rows back
+ * to back; the context's own row map addresses a whole frame (WCPT_OPTION_GATHER_FRAME_ROWS). */
+
+/* :323 imageStore of pixel (lx, ly) of the context's rows into the accumulation image (index i = ly * W + lx), and
+ * into the gather output (wcpt_set_gather_output) at row frame_row(wm, ly) of that output */
 __device__ __forceinline__ void store_pixel(float4* __restrict__ image, float* __restrict__ wire, uint32_t wire_ch,
-                                            size_t i, f3 acc)
+                                            const RowMap& wm, uint32_t W, uint32_t lx, uint32_t ly, f3 acc)
 {
+    const size_t i = (size_t)ly * W + lx;
     image[i] = make_float4(acc.x, acc.y, acc.z, 1.0f);
     if (wire) {
+        const size_t j = (size_t)frame_row(wm, ly) * W + lx;
         if (wire_ch == 3u) {
-            float* w = wire + 3u * i;
+            float* w = wire + 3u * j;
             w[0] = acc.x;
             w[1] = acc.y;
             w[2] = acc.z;
         } else if (wire_ch == 4u) {
-            reinterpret_cast<float4*>(wire)[i] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+            reinterpret_cast<float4*>(wire)[j] = make_float4(acc.x, acc.y, acc.z, 1.0f);
         } else {
-            reinterpret_cast<uint32_t*>(wire)[i] = display_rgba8(acc);
+            reinterpret_cast<uint32_t*>(wire)[j] = display_rgba8(acc);
         }
     }
 }

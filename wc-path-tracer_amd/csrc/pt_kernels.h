@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "../../include/wcpt.h"
+#include "row_map.h"
 
 namespace wcpt {
 
@@ -38,6 +39,9 @@ struct LaunchArgs {
     float* wire;                 /* gather payload (wcpt_set_gather_output) or null */
     uint32_t wire_ch;            /* its format (wcpt.h WCPT_PAYLOAD_*): 3 = RGB32F (12 B/px), 4 = RGBA32F (16 B/px), 8 = display RGBA8 (4 B/px) */
     uint32_t W, H, y0, rows;
+    /* frame row of local row ly: y0 + ly + (ly >> row_shift) * row_gap (row_map.h; contiguous: 31, 0) */
+    uint32_t row_shift = kContiguousShift, row_gap = 0;
+    RowMap wire_rows = {0, kContiguousShift, 0}; /* the gather output's row of local row ly (row_map.h) */
     uint32_t* status;
     unsigned long long* counters;
 };
@@ -67,6 +71,7 @@ struct WfBuffers {
     unsigned long long* diag; /* DIAG builds: trace-loop phase timers (8 x u64)         */
     float* wire;       /* gather payload (LaunchArgs::wire) or null                     */
     uint32_t wire_ch;
+    RowMap wire_rows;  /* LaunchArgs::wire_rows                                         */
 };
 /* One pipeline's path state, sized by the pipeline's own path count (its share of the 8x8 tiles), not the frame:
  * the slot arrays hold only the paths that pipeline can have live at once. The per-pixel sample sums are shared
@@ -118,6 +123,7 @@ struct MkState {
     void* temp = nullptr;
     size_t temp_bytes = 0;
     uint32_t geom_w = 0, geom_rows = 0, geom_y0 = 0, geom_tiles = 0; /* geometry the costs and order belong to */
+    uint32_t geom_shift = kContiguousShift, geom_gap = 0;            /* ... and its frame rows (row_map.h) */
     uint32_t renders = 0;      /* renders of that geometry */
     bool order_valid = false;
 };
@@ -168,7 +174,9 @@ int context_device(wcpt_context* ctx);
 int context_error(wcpt_context* ctx, int code, const char* msg);
 int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                     uint64_t draws);
-int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows);
+/* CreateScreen of one context's rows: a block [y0, y0 + rows), or (stripe > 0) interleaved stripes (row_map.h) */
+int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows, uint32_t stripe = 0,
+                    uint32_t period = 0);
 void render_abandon(wcpt_context* ctx);
 
 } // namespace wcpt

@@ -70,10 +70,10 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
                                             const wcpt_draw_command* __restrict__ draws,
                                             const uint64_t* __restrict__ tri_records, float4* __restrict__ image,
                                             float* __restrict__ wire, uint32_t wire_ch,
-                                            uint32_t W, uint32_t H, uint32_t y0, uint32_t lx, uint32_t ly, Stack& stk,
-                                            Counters& cnt, bool& overflow)
+                                            uint32_t W, uint32_t H, const RowMap& rm, const RowMap& wm, uint32_t lx,
+                                            uint32_t ly, Stack& stk, Counters& cnt, bool& overflow)
 {
-    const uint32_t x = lx, y = y0 + ly;
+    const uint32_t x = lx, y = frame_row(rm, ly); /* the frame row: a row block or interleaved stripes (row_map.h) */
     const f3 dir = primary_direction(sd, x, y, W, H);
     const uint32_t pixel_index = x + y * W + sd.renderedFramesCount * 719393u; /* :304 */
     uint32_t seed = pcg_hash(pixel_index);
@@ -105,7 +105,7 @@ __device__ __forceinline__ void shade_pixel(const wcpt_scene_data& sd, const wcp
             const float iw = 1.0f - weight;
             acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight, o.z * iw + result.z * weight);
         }
-        store_pixel(image, wire, wire_ch, (size_t)ly * W + lx, acc); /* :323 */
+        store_pixel(image, wire, wire_ch, wm, W, lx, ly, acc); /* :323 */
     }
     if (COUNT) cnt.pixels++;
     phase_mark(cnt, 6);
@@ -123,8 +123,8 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
                                                     const wcpt_draw_command* __restrict__ draws,
                                                     const uint64_t* __restrict__ tri_records,
                                                     float4* __restrict__ image, float* __restrict__ wire,
-                                                    uint32_t wire_ch, uint32_t W, uint32_t H, uint32_t y0,
-                                                    uint32_t rows, uint32_t tilesX, uint32_t tilesTotal,
+                                                    uint32_t wire_ch, uint32_t W, uint32_t H, const RowMap rm,
+                                                    const RowMap wm, uint32_t rows, uint32_t tilesX, uint32_t tilesTotal,
                                                     uint32_t scatter, const uint32_t* __restrict__ tile_order,
                                                     uint32_t* __restrict__ tile_cost, uint32_t* __restrict__ status,
                                                     unsigned long long* __restrict__ counters)
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
             uint64_t mem[kPrivateStack];
             PrivateStack<kPrivateStack> stk;
             stk.mem = (priv_u64_ptr)mem;
-            shade_pixel<COUNT, DIAG, PAIRS, SINGLE, REUSE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
+            shade_pixel<COUNT, DIAG, PAIRS, SINGLE, REUSE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, rm, wm, lx, ly, stk,
                                             cnt, overflow);
         } else {
             __shared__ uint64_t s_stack[kLdsStack * 64];
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(64, WCPT_MK_WAVES) void pt_megakernel(const wcpt_sc
             LdsStack<kLdsStack, kSpillStack> stk;
             stk.base = (lds_u64_ptr)(s_stack + (threadIdx.x & 63u));
             stk.spill = (priv_u64_ptr)spill;
-            shade_pixel<COUNT, DIAG, PAIRS, SINGLE, REUSE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, y0, lx, ly, stk,
+            shade_pixel<COUNT, DIAG, PAIRS, SINGLE, REUSE>(sd, mats, spheres, draws, tri_records, image, wire, wire_ch, W, H, rm, wm, lx, ly, stk,
                                             cnt, overflow);
         }
     }
@@ -435,8 +435,8 @@ static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stre
      * a sort (launch_megakernel) take the tiles longest first */
     const bool cost_order = !COUNT && a.mk_tile_order == 2 && mk.cost != nullptr;
     hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE, REUSE>), dim3(tiles), dim3(64), 0, stream, a.sd,
-                       a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H, a.y0,
-                       a.rows, tilesX, tiles, scatter, cost_order && mk.order_valid ? mk.order : nullptr,
+                       a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H,
+                       RowMap{a.y0, a.row_shift, a.row_gap}, a.wire_rows, a.rows, tilesX, tiles, scatter, cost_order && mk.order_valid ? mk.order : nullptr,
                        cost_order ? mk.cost : nullptr, a.status, a.counters);
     return hipGetLastError();
 }
@@ -493,11 +493,14 @@ static hipError_t cost_order_prepare(const LaunchArgs& a, MkState& mk, uint32_t 
         mk.cap = tiles;
         mk.geom_tiles = 0; /* forces the reset below */
     }
-    if (mk.geom_tiles != tiles || mk.geom_w != a.W || mk.geom_rows != a.rows || mk.geom_y0 != a.y0) {
+    if (mk.geom_tiles != tiles || mk.geom_w != a.W || mk.geom_rows != a.rows || mk.geom_y0 != a.y0 ||
+        mk.geom_shift != a.row_shift || mk.geom_gap != a.row_gap) {
         mk.geom_tiles = tiles;
         mk.geom_w = a.W;
         mk.geom_rows = a.rows;
         mk.geom_y0 = a.y0;
+        mk.geom_shift = a.row_shift;
+        mk.geom_gap = a.row_gap;
         mk.renders = 0;
         mk.order_valid = false;
         return hipMemsetAsync(mk.cost, 0, (size_t)tiles * 4u, stream); /* the running averages start at 0 */

@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
 template <bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd, const wcpt_sphere* __restrict__ spheres,
                                                        WfBuffers b, float4* __restrict__ image,
-                                                       uint32_t W, uint32_t H, uint32_t y0, uint32_t rows,
+                                                       uint32_t W, uint32_t H, const RowMap rm, uint32_t rows,
                                                        uint32_t tilesX, uint32_t total, uint32_t pipe, uint32_t npipes,
                                                        unsigned long long* __restrict__ counters)
 {
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
             const uint32_t ly = (t / tilesX) * 8u + (q >> 3);
             if (lx < W && ly < rows) {
                 p = ly * W + lx;
-                const uint32_t y = y0 + ly;
+                const uint32_t y = frame_row(rm, ly); /* row block or interleaved stripes (row_map.h) */
                 seed = pcg_hash(lx + y * W + sd.renderedFramesCount * 719393u); /* :304-305 */
                 b.result[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 if (sd.samples > 0) {
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
                     live = true;
                 } else { /* samples == 0: result / 0 = NaN (:312), stored as the reference would */
                     const f3 r = mk3(0.0f, 0.0f, 0.0f) / (float)sd.samples;
-                    if (!COUNT) store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, r);
+                    if (!COUNT) store_pixel(image, b.wire, b.wire_ch, b.wire_rows, W, lx, ly, r);
                     if (COUNT) cnt.pixels++;
                 }
             }
@@ -616,7 +616,7 @@ void wf_trace(const wcpt_scene_data sd, const wcpt_draw_command* __restrict__ dr
                             acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight,
                                       o.z * iw + result.z * weight);
                         }
-                        store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, acc); /* :323 */
+                        store_pixel(image, b.wire, b.wire_ch, b.wire_rows, W, lx, ly, acc); /* :323 */
                         mode = kModeIdle;
                     }
                 }
@@ -662,7 +662,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
                                                         const wcpt_draw_command* __restrict__ draws,
                                                         const uint64_t* __restrict__ tri_records, WfBuffers b,
                                                         float4* __restrict__ image, uint32_t W,
-                                                        uint32_t H, uint32_t y0, unsigned long long* __restrict__ counters)
+                                                        uint32_t H, const RowMap rm, unsigned long long* __restrict__ counters)
 {
     __shared__ uint32_t s_wave[kShadeBlock / 64], s_base;
     if (blockIdx.x == 0 && threadIdx.x == 0) *b.head = 0; /* the trace of this iteration has finished */
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
                 const uint32_t lx = p % W, ly = p / W;
                 if (sample < sd.samples) {                                  /* next sample, same primary ray */
                     path_begin(ps, mk3(sd.position[0], sd.position[1], sd.position[2]),
-                               primary_direction(sd, lx, y0 + ly, W, H));
+                               primary_direction(sd, lx, frame_row(rm, ly), W, H));
                     if (!reuse) {
                         cont = true;
                         break;
@@ -747,7 +747,7 @@ __global__ __launch_bounds__(kShadeBlock) void wf_shade(const wcpt_scene_data sd
                         acc = mk3(o.x * iw + result.x * weight, o.y * iw + result.y * weight,
                                   o.z * iw + result.z * weight);
                     }
-                    store_pixel(image, b.wire, b.wire_ch, (size_t)ly * W + lx, acc); /* :323 */
+                    store_pixel(image, b.wire, b.wire_ch, b.wire_rows, W, lx, ly, acc); /* :323 */
                 }
                 if (COUNT) cnt.pixels++;
                 break;
@@ -925,7 +925,7 @@ static void wf_iteration(const LaunchArgs& a, const WfBuffers& b, uint32_t trace
     hipLaunchKernelGGL((dev::wf_trace<COUNT, DIAG, GEO, LDSN>), dim3(trace_grid), dim3(64), 0, stream, a.sd, a.draws,
                        a.tri_records, b, a.status, a.counters, a.wf_refill, a.materials, a.spheres, a.image, a.W, a.H);
     hipLaunchKernelGGL(dev::wf_shade<COUNT>, dim3(shade_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.materials,
-                       a.spheres, a.draws, a.tri_records, b, a.image, a.W, a.H, a.y0, a.counters);
+                       a.spheres, a.draws, a.tri_records, b, a.image, a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.counters);
 }
 
 template <bool COUNT, bool DIAG, int GEO, int LDSN>
@@ -1048,15 +1048,16 @@ static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const Wf
     }
     b.wire = a.wire;
     b.wire_ch = a.wire_ch;
+    b.wire_rows = a.wire_rows;
     b.count_in = s.ctr + 0;
     b.count_out = s.ctr + 1;
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);
     if (count)
         hipLaunchKernelGGL(dev::wf_init<true>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
-                           a.W, a.H, a.y0, a.rows, tilesX, total, pipe, npipes, a.counters);
+                           a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.rows, tilesX, total, pipe, npipes, a.counters);
     else
         hipLaunchKernelGGL(dev::wf_init<false>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
-                           a.W, a.H, a.y0, a.rows, tilesX, total, pipe, npipes, a.counters);
+                           a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.rows, tilesX, total, pipe, npipes, a.counters);
     return hipGetLastError();
 }
 

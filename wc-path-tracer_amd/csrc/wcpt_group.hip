@@ -73,6 +73,8 @@ struct LocalRank {
     hipEvent_t sent[kPayloadBuffers] = {};   /* the transfer that read payload[b] has finished */
     bool sent_pending[kPayloadBuffers] = {};
     std::vector<void*> retired;              /* replaced payload buffers, freed at the next group-wide wait */
+    void* stage = nullptr;                   /* root, RCCL with row stripes: every sender's block back to back */
+    uint64_t stage_cap = 0;
 };
 
 #if WCPT_GROUP_TIMERS
@@ -133,6 +135,8 @@ struct wcpt_group {
     /* WCPT_GROUP_OPTION_TIMEOUT_MS: -1 (default) = kDefaultTimeoutMs in a group of several ranks, none in a group of
      * one; 0 = wait forever */
     int timeout_ms = -1;
+    /* WCPT_GROUP_OPTION_ROW_STRIPE: rows per interleaved stripe, 0 = contiguous row blocks */
+    uint32_t stripe = 0;
     std::vector<std::unique_ptr<Worker>> workers; /* local ranks 1..n-1 (the caller's thread issues local rank 0) */
     std::atomic<bool> stopping{false};
     std::atomic<uint32_t> done{0};
@@ -182,9 +186,30 @@ bool valid_format(int f)
     return f == WCPT_PAYLOAD_RGB32F || f == WCPT_PAYLOAD_RGBA32F || f == WCPT_PAYLOAD_DISPLAY_RGBA8;
 }
 
+/* rank's rows: a contiguous block, or its first stripe's row and its row count (WCPT_GROUP_OPTION_ROW_STRIPE) */
 void block_of(const wcpt_group* g, int rank, uint32_t& y0, uint32_t& rows)
 {
-    (void)wcpt_row_block(g->height, (uint32_t)g->nranks, (uint32_t)rank, &y0, &rows);
+    (void)wcpt_row_stripes(g->height, (uint32_t)g->nranks, (uint32_t)rank, g->stripe, &y0, &rows);
+}
+
+/* Where rank's `rows` rows sit in the frame relative to its first (row_map.h): stripes of g->stripe rows every
+ * nranks * stripe rows. Rank `rank`'s rows, back to back at `src` (px bytes per pixel), to their rows of `frame`:
+ * one 2D copy of its whole stripes (pitch nranks * stripe rows in the frame, stripe rows at the source) and one copy
+ * of its short last stripe, if it holds one. hipMemcpyDefault: the source may be another device's memory (COPY). */
+hipError_t copy_stripes(const wcpt_group* g, int rank, void* frame, const void* src, uint64_t px, hipStream_t s)
+{
+    uint32_t y0 = 0, rows = 0;
+    block_of(g, rank, y0, rows);
+    const uint64_t row = (uint64_t)g->width * px;
+    const uint64_t S = g->stripe, P = S * (uint64_t)g->nranks;
+    const uint64_t full = rows / S, tail = rows % S;
+    char* dst = static_cast<char*>(frame) + (uint64_t)y0 * row;
+    hipError_t e = hipSuccess;
+    if (full) e = hipMemcpy2DAsync(dst, P * row, src, S * row, S * row, full, hipMemcpyDefault, s);
+    if (e == hipSuccess && tail)
+        e = hipMemcpyAsync(dst + full * P * row, static_cast<const char*>(src) + full * S * row, tail * row,
+                           hipMemcpyDefault, s);
+    return e;
 }
 
 bool presenting(const wcpt_group* g) { return g->format != 0 && g->width != 0; }
@@ -213,8 +238,10 @@ void free_retired(LocalRank& lr)
 int attach_payloads(wcpt_group* g)
 {
     for (LocalRank& lr : g->local) {
+        int rc = wcpt_set_option(lr.ctx, WCPT_OPTION_GATHER_FRAME_ROWS, 0);
+        if (rc) return rc;
         if (!presenting(g)) {
-            const int rc = wcpt_set_gather_output(lr.ctx, 0, 0, 0);
+            rc = wcpt_set_gather_output(lr.ctx, 0, 0, 0);
             if (rc) return rc;
             continue;
         }
@@ -223,9 +250,33 @@ int attach_payloads(wcpt_group* g)
         const uint64_t bytes = (uint64_t)g->width * rows * pixel_bytes(g->format);
         if (lr.rank == g->root || g->transport == WCPT_GROUP_TRANSPORT_DIRECT) {
             /* the root renders into its rows of the frame; with the DIRECT transport every rank does, over xGMI */
-            const int rc = wcpt_set_gather_output(lr.ctx, g->dst + (uint64_t)g->width * y0 * pixel_bytes(g->format),
-                                                  bytes, (uint32_t)g->format);
+            if (g->stripe) {
+                /* interleaved stripes: the output is the whole frame, addressed by frame row */
+                rc = wcpt_set_option(lr.ctx, WCPT_OPTION_GATHER_FRAME_ROWS, 1);
+                if (!rc) rc = wcpt_set_gather_output(lr.ctx, g->dst, g->dst_bytes, (uint32_t)g->format);
+            } else {
+                rc = wcpt_set_gather_output(lr.ctx, g->dst + (uint64_t)g->width * y0 * pixel_bytes(g->format), bytes,
+                                            (uint32_t)g->format);
+            }
             if (rc) return rc;
+            if (lr.rank == g->root && g->stripe && g->transport == WCPT_GROUP_TRANSPORT_RCCL && g->nranks > 1) {
+                /* the senders' blocks arrive back to back in the staging buffer, then go to their rows (kScatter) */
+                const uint64_t need = (uint64_t)g->width * (g->height - rows) * pixel_bytes(g->format);
+                if (lr.stage_cap < need) {
+                    GHIP(hipSetDevice(lr.device), "hipSetDevice");
+                    if (lr.stage) lr.retired.push_back(lr.stage);
+                    lr.stage = nullptr;
+                    lr.stage_cap = 0;
+                    const hipError_t e = hipMalloc(&lr.stage, need);
+                    if (e != hipSuccess) {
+                        lr.stage = nullptr;
+                        (void)hipGetLastError();
+                        return group_error(WCPT_ERROR_OUT_OF_DEVICE_MEMORY, "hipMalloc(staging of the root, %llu bytes): %s",
+                                           (unsigned long long)need, hipGetErrorString(e));
+                    }
+                    lr.stage_cap = need;
+                }
+            }
             continue;
         }
         GHIP(hipSetDevice(lr.device), "hipSetDevice");
@@ -242,8 +293,7 @@ int attach_payloads(wcpt_group* g)
             lr.payload_cap[b] = bytes;
         }
         /* the next render picks its buffer; park the output on buffer 0 meanwhile */
-        const int rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[0]), bytes,
-                                              (uint32_t)g->format);
+        rc = wcpt_set_gather_output(lr.ctx, reinterpret_cast<uint64_t>(lr.payload[0]), bytes, (uint32_t)g->format);
         if (rc) return rc;
     }
     return WCPT_SUCCESS;
@@ -338,6 +388,14 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
         block_of(g, rank, y0, rows);
         return reinterpret_cast<void*>(g->dst + (uint64_t)g->width * y0 * px);
     };
+    /* row stripes, RCCL: where rank `peer`'s block lands in the root's staging buffer (the senders' blocks in rank
+     * order, back to back) */
+    auto stage_of = [&](const LocalRank& rt, int peer) {
+        uint64_t off = 0;
+        for (int r = 0; r < peer; r++)
+            if (r != g->root) off += block_bytes(r);
+        return static_cast<void*>(static_cast<char*>(rt.stage) + off);
+    };
     /* 2-5 may fail only on a device or transport error. Once the plan has started, ranks (and, in a group of several
      * processes, the peers posting their part of this frame's exchange) are out of step, so any failure breaks the
      * group -- the same rule for a failing hipEventRecord / hipStreamWaitEvent / copy as for a failing render. */
@@ -394,6 +452,11 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
             if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
                 const LocalRank& rt = g->local[g->root_local]; /* the COPY transport is single-process */
                 PHIP(hipSetDevice(lr.device), "hipSetDevice");
+                if (g->stripe) {
+                    PHIP(copy_stripes(g, lr.rank, reinterpret_cast<void*>(g->dst), lr.payload[st.buffer], px,
+                                      stream_of(lr, st.stream)), "hipMemcpy2DAsync(stripes)");
+                    break;
+                }
                 PHIP(hipMemcpyPeerAsync(frame_rows(lr.rank), rt.device, lr.payload[st.buffer], lr.device,
                                         block_bytes(lr.rank), stream_of(lr, st.stream)),
                      "hipMemcpyPeerAsync(block)");
@@ -412,10 +475,15 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
                                     stream_of(lr, st.stream));
                 xfer_what = "ncclSend";
             } else {
-                xfer_err = ncclRecv(frame_rows(st.peer), block_bytes(st.peer), ncclUint8, st.peer, lr.comm,
-                                    stream_of(lr, st.stream));
+                xfer_err = ncclRecv(g->stripe ? stage_of(lr, st.peer) : frame_rows(st.peer), block_bytes(st.peer),
+                                    ncclUint8, st.peer, lr.comm, stream_of(lr, st.stream));
                 xfer_what = "ncclRecv";
             }
+            break;
+        case plan::kScatter:
+            PHIP(hipSetDevice(lr.device), "hipSetDevice");
+            PHIP(copy_stripes(g, st.peer, reinterpret_cast<void*>(g->dst), stage_of(lr, st.peer), px,
+                              stream_of(lr, st.stream)), "hipMemcpy2DAsync(received stripes)");
             break;
         case plan::kRecordSent:
             PHIP(hipSetDevice(lr.device), "hipSetDevice");
@@ -798,6 +866,7 @@ int wcpt_group_destroy(wcpt_group* g)
             if (lr.ready[b]) (void)hipEventDestroy(lr.ready[b]);
             if (lr.sent[b]) (void)hipEventDestroy(lr.sent[b]);
         }
+        if (lr.stage) (void)hipFree(lr.stage);
         free_retired(lr);
         if (lr.comm_stream) {
             (void)hipStreamSynchronize(lr.comm_stream);
@@ -828,9 +897,40 @@ int wcpt_row_block(uint32_t height, uint32_t n, uint32_t rank, uint32_t* y0, uin
     return WCPT_SUCCESS;
 }
 
+int wcpt_row_stripes(uint32_t height, uint32_t n, uint32_t rank, uint32_t stripe, uint32_t* y_first, uint32_t* rows)
+{
+    if (stripe == 0) return wcpt_row_block(height, n, rank, y_first, rows);
+    if (!y_first || !rows || n == 0 || rank >= n || (stripe & (stripe - 1u))) return WCPT_ERROR_INVALID_ARGUMENT;
+    /* stripes s = rank, rank + n, ... below T = ceil(height / stripe); only the frame's last stripe can be short */
+    const uint64_t T = ((uint64_t)height + stripe - 1u) / stripe;
+    const uint64_t count = T > rank ? (T - 1u - rank) / n + 1u : 0u;
+    uint64_t r = count * stripe;
+    if (count && (T - 1u - rank) % n == 0 && height % stripe) r -= stripe - height % stripe; /* it holds the short one */
+    *y_first = rank * stripe;
+    *rows = (uint32_t)r;
+    return WCPT_SUCCESS;
+}
+
 int wcpt_group_set_option(wcpt_group* g, int option, int value)
 {
     if (!g) return group_error(WCPT_ERROR_INVALID_HANDLE, "null group");
+    if (option == WCPT_GROUP_OPTION_ROW_STRIPE) {
+        if (value < 0 || value > 32768 || (value & (value - 1)))
+            return group_error(WCPT_ERROR_INVALID_ARGUMENT, "row stripe %d (0, or a power of two up to 32768)", value);
+        if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
+        const int rc = wcpt_group_sync(g); /* queued frames keep the split they were issued with */
+        if (rc) return rc;
+        const uint32_t old = g->stripe;
+        g->stripe = (uint32_t)value;
+        if (g->width && old != g->stripe) {
+            const int rc2 = wcpt_group_create_screen(g, g->width, g->height); /* lay the frame out again */
+            if (rc2) {
+                if (!g->broken) g->stripe = old;
+                return rc2;
+            }
+        }
+        return WCPT_SUCCESS;
+    }
     if (option == WCPT_GROUP_OPTION_TIMEOUT_MS) {
         if (value < 0) return group_error(WCPT_ERROR_INVALID_ARGUMENT, "group timeout %d ms (>= 0; 0 = none)", value);
         g->timeout_ms = value;
@@ -885,6 +985,9 @@ int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
     if (g->broken) return group_error(WCPT_ERROR_DEVICE_LOST, "group aborted after a transport failure");
     if (width == 0 || height < (uint32_t)g->nranks) /* the same decision in every process */
         return group_error(WCPT_ERROR_INVALID_ARGUMENT, "%ux%u frame for %d row blocks", width, height, g->nranks);
+    if (g->stripe && ((uint64_t)height + g->stripe - 1u) / g->stripe < (uint64_t)g->nranks)
+        return group_error(WCPT_ERROR_INVALID_ARGUMENT, "%ux%u frame: fewer stripes of %u rows than %d ranks", width,
+                           height, g->stripe, g->nranks);
     const uint32_t old_w = g->width, old_h = g->height;
     g->width = width;
     g->height = height;
@@ -893,7 +996,8 @@ int wcpt_group_create_screen(wcpt_group* g, uint32_t width, uint32_t height)
          * block are set in one step, so no rank ever allocates more than its block (zeroed: CreateScreen) */
         uint32_t y0 = 0, rows = 0;
         block_of(g, lr.rank, y0, rows);
-        const int rc = wcpt::set_frame_block(lr.ctx, width, height, y0, rows);
+        const int rc = wcpt::set_frame_block(lr.ctx, width, height, y0, rows, g->stripe,
+                                             g->stripe * (uint32_t)g->nranks);
         if (rc) {
             g->width = old_w;
             g->height = old_h;
@@ -996,7 +1100,8 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
         g->plan_state[i].rank = g->local[i].rank;
         for (int k = 0; k < kPayloadBuffers; k++) g->plan_state[i].sent_pending[k] = g->local[i].sent_pending[k];
     }
-    plan::frame_steps(g->nranks, g->root, g->overlap, exchange, g->transport, g->frames, g->plan_state, g->steps);
+    plan::frame_steps(g->nranks, g->root, g->overlap, exchange, g->transport, g->frames, g->plan_state, g->steps,
+                      g->stripe != 0);
     return issue_frame(g, scene, materials, spheres, draw_commands, exchange);
 }
 

@@ -136,7 +136,9 @@ struct wcpt_context {
     uint64_t wire_bytes = 0;
     uint32_t wire_ch = 3;
     uint32_t width = 0, height = 0, y0 = 0, rows = 0; /* rows == height when not sharded */
+    uint32_t stripe = 0, period = 0;   /* wcpt_set_row_stripes (0: a contiguous block [y0, y0 + rows)) */
     bool sharded = false;
+    int gather_frame_rows = 0;         /* WCPT_OPTION_GATHER_FRAME_ROWS */
     uint32_t* d_status = nullptr;
     unsigned long long* d_counters = nullptr;
     wcpt::WfPipes wf;                  /* path state + streams of the wavefront pipelines (allocated on first use) */
@@ -271,6 +273,16 @@ int alloc_image(wcpt_context* ctx, uint32_t w, uint32_t h, uint32_t y0, uint32_t
     ctx->rows = rows;
     return WCPT_SUCCESS;
 }
+
+/* The context's row map (row_map.h): frame row of each local row. */
+wcpt::RowMap row_map(const wcpt_context* ctx)
+{
+    if (!ctx->stripe) return {ctx->y0, wcpt::kContiguousShift, 0u};
+    return {ctx->y0, (uint32_t)__builtin_ctz(ctx->stripe), ctx->period - ctx->stripe};
+}
+
+/* The frame row of the context's last local row (its rows must be > 0). */
+uint64_t last_frame_row(const wcpt_context* ctx) { return wcpt::frame_row64(row_map(ctx), ctx->rows - 1u); }
 
 /* The buffer whose [ptr, ptr + bytes) contains device address `addr`, or null. */
 Buffer* buffer_at(wcpt_context* ctx, uint64_t addr, uint64_t& offset)
@@ -518,10 +530,12 @@ int check_render_args(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t 
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: drawCommandCount > 0 with null draw commands");
     if (materials == 0 && (scene->sphereCount > 0 || scene->drawCommandCount > 0))
         return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "wcpt_render: null material buffer");
+    /* the output's rows: the context's rows back to back, or (WCPT_OPTION_GATHER_FRAME_ROWS) frame rows up to its last */
+    const uint64_t wire_rows = ctx->gather_frame_rows ? last_frame_row(ctx) + 1u : ctx->rows;
     if (ctx->wire && mode == wcpt::kModeRender &&
-        (uint64_t)ctx->width * ctx->rows * payload_pixel_bytes(ctx->wire_ch) > ctx->wire_bytes)
-        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%u x %u B",
-                         (unsigned long long)ctx->wire_bytes, ctx->width, ctx->rows,
+        (uint64_t)ctx->width * wire_rows * payload_pixel_bytes(ctx->wire_ch) > ctx->wire_bytes)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather output of %llu bytes too small for %ux%llu x %u B",
+                         (unsigned long long)ctx->wire_bytes, ctx->width, (unsigned long long)wire_rows,
                          (unsigned)payload_pixel_bytes(ctx->wire_ch));
     return WCPT_SUCCESS;
 }
@@ -546,6 +560,12 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.H = ctx->height;
     a.y0 = ctx->y0;
     a.rows = ctx->rows;
+    {
+        const wcpt::RowMap m = row_map(ctx);
+        a.row_shift = m.shift;
+        a.row_gap = m.gap;
+        a.wire_rows = ctx->gather_frame_rows ? m : wcpt::RowMap{0u, wcpt::kContiguousShift, 0u};
+    }
     a.status = ctx->d_status;
     a.counters = ctx->d_counters;
     a.tri_records = nullptr;
@@ -690,15 +710,22 @@ int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t ma
 
 /* CreateScreen of one row block in one step: the frame's size and the context's block [y0, y0 + rows) are set
  * together, so only the block is allocated (and zeroed), whatever the previous frame's size was. */
-int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows)
+int set_frame_block(wcpt_context* ctx, uint32_t width, uint32_t height, uint32_t y0, uint32_t rows, uint32_t stripe,
+                    uint32_t period)
 {
     int rc = bind(ctx);
     if (rc) return rc;
-    if (width == 0 || rows == 0 || (uint64_t)y0 + rows > height)
-        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "row block [%u,%u) of a %ux%u frame", y0, y0 + rows, width,
-                         height);
+    if (stripe && (stripe & (stripe - 1u) || stripe > 32768u || period < stripe))
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "row stripes of %u rows every %u rows", stripe, period);
+    const uint64_t last = rows == 0 ? 0 : frame_row64(wcpt::RowMap{y0, stripe ? (uint32_t)__builtin_ctz(stripe) : kContiguousShift,
+                                                                 stripe ? period - stripe : 0u}, rows - 1u);
+    if (width == 0 || rows == 0 || last >= height)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "%u rows from row %u (stripes %u / %u) in a %ux%u frame", rows,
+                         y0, stripe, period, width, height);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     ctx->sharded = true;
+    ctx->stripe = stripe;
+    ctx->period = stripe ? period : 0u;
     rc = alloc_image(ctx, width, height, y0, rows);
     if (rc) return rc;
     if (!ctx->external_bytes) {
@@ -902,6 +929,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
         if (value < 0 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "stack kind %d", value);
         ctx->stack_kind = value;
         return WCPT_SUCCESS;
+    case WCPT_OPTION_GATHER_FRAME_ROWS:
+        if (value < 0 || value > 1) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "gather frame rows %d", value);
+        ctx->gather_frame_rows = value;
+        return WCPT_SUCCESS;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "unknown option %d", option);
     }
 }
@@ -1030,7 +1061,16 @@ int wcpt_create_screen(wcpt_context* ctx, uint32_t width, uint32_t height)
     if (width == 0 || height == 0) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "zero-sized screen");
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     uint32_t y0 = 0, rows = height;
-    if (ctx->sharded && ctx->y0 < height) {
+    if (ctx->sharded && ctx->stripe) {
+        /* interleaved stripes: kept while every row still lies in the new frame, else the full frame */
+        if (ctx->rows && last_frame_row(ctx) < height) {
+            y0 = ctx->y0;
+            rows = ctx->rows;
+        } else {
+            ctx->sharded = false;
+            ctx->stripe = ctx->period = 0;
+        }
+    } else if (ctx->sharded && ctx->y0 < height) {
         y0 = ctx->y0;
         rows = (ctx->y0 + ctx->rows <= height) ? ctx->rows : height - ctx->y0;
     } else {
@@ -1058,6 +1098,7 @@ int wcpt_set_row_range(wcpt_context* ctx, uint32_t y0, uint32_t rows)
     if (rc) return rc;
     if (rows == 0) {
         ctx->sharded = false;
+        ctx->stripe = ctx->period = 0;
         if (ctx->height) return alloc_image(ctx, ctx->width, ctx->height, 0, ctx->height);
         return WCPT_SUCCESS;
     }
@@ -1066,9 +1107,34 @@ int wcpt_set_row_range(wcpt_context* ctx, uint32_t y0, uint32_t rows)
                          ctx->height);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     ctx->sharded = true;
+    ctx->stripe = ctx->period = 0;
     ctx->y0 = y0;
     ctx->rows = rows;
     if (ctx->height) return alloc_image(ctx, ctx->width, ctx->height, y0, rows);
+    return WCPT_SUCCESS;
+}
+
+int wcpt_set_row_stripes(wcpt_context* ctx, uint32_t y_first, uint32_t rows, uint32_t stripe, uint32_t period)
+{
+    if (stripe == 0) return wcpt_set_row_range(ctx, y_first, rows);
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (rows == 0 || stripe & (stripe - 1u) || stripe > 32768u || period < stripe)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "%u rows in stripes of %u rows every %u rows", rows, stripe,
+                         period);
+    const uint64_t last = wcpt::frame_row64(wcpt::RowMap{y_first, (uint32_t)__builtin_ctz(stripe), period - stripe}, rows - 1u);
+    if (ctx->height && last >= ctx->height)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "row stripes reach row %llu of a frame of height %u",
+                         (unsigned long long)last, ctx->height);
+    if (last > 0xFFFFFFFFull)
+        return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "row stripes past row 2^32");
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    ctx->sharded = true;
+    ctx->stripe = stripe;
+    ctx->period = period;
+    ctx->y0 = y_first;
+    ctx->rows = rows;
+    if (ctx->height) return alloc_image(ctx, ctx->width, ctx->height, y_first, rows);
     return WCPT_SUCCESS;
 }
 

@@ -55,6 +55,7 @@ OPTION_WF_PIPES = 10
 OPTION_PROFILE_REGION = 11
 OPTION_WF_FETCH = 12
 OPTION_WF_PERSIST = 13
+OPTION_GATHER_FRAME_ROWS = 14
 DEFAULT_WF_PIPES = 0  # wcpt_runtime.hip: by queue length (2 or 3)
 
 # gather payload formats (wcpt_set_gather_output, wcpt_group_set_output)
@@ -92,6 +93,7 @@ GROUP_UNIQUE_ID_BYTES = 128
 GROUP_OPTION_OVERLAP = 1
 GROUP_OPTION_THREADS = 2
 GROUP_OPTION_TIMEOUT_MS = 3
+GROUP_OPTION_ROW_STRIPE = 4
 ABI_VERSION = 4
 assert SCENE_DATA_DTYPE.itemsize == 164 and MATERIAL_DTYPE.itemsize == 60 and SPHERE_DTYPE.itemsize == 20
 assert NODE_DTYPE.itemsize == 32 and DRAW_COMMAND_DTYPE.itemsize == 32
@@ -161,6 +163,7 @@ _PROTOTYPES = {
     "wcpt_create_screen": (_i, [_p, _u32, _u32]),
     "wcpt_resize": (_i, [_p, _u32, _u32]),
     "wcpt_set_row_range": (_i, [_p, _u32, _u32]),
+    "wcpt_set_row_stripes": (_i, [_p, _u32, _u32, _u32, _u32]),
     "wcpt_image_device_ptr": (_u64, [_p]),
     "wcpt_set_external_image": (_i, [_p, _u64, _u64]),
     "wcpt_set_gather_output": (_i, [_p, _u64, _u64, _u32]),
@@ -186,6 +189,7 @@ _PROTOTYPES = {
     "wcpt_selftest_device": (_i, [_p, _i, _p, _p, _p, _u32]),
     "wcpt_runtime_version": (_i, [C.POINTER(_i)]),
     "wcpt_row_block": (_i, [_u32, _u32, _u32, C.POINTER(_u32), C.POINTER(_u32)]),
+    "wcpt_row_stripes": (_i, [_u32, _u32, _u32, _u32, C.POINTER(_u32), C.POINTER(_u32)]),
     "wcpt_group_create": (_i, [C.POINTER(_i), _i, _i, C.POINTER(_p)]),
     "wcpt_group_destroy": (_i, [_p]),
     "wcpt_group_context": (_p, [_p, _i]),

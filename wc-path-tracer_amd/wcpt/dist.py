@@ -21,6 +21,31 @@ def row_block(height: int, world: int, rank: int) -> tuple[int, int]:
     return y0, y1 - y0
 
 
+def row_stripes(height: int, world: int, rank: int, stripe: int = 0) -> tuple[int, int]:
+    """(y_first, rows) of `rank` under interleaved stripes of `stripe` rows (include/wcpt.h wcpt_row_stripes): rank r
+    takes stripes r, r + world, ... of ceil(height / stripe); only the frame's last stripe can be short. stripe 0 is
+    row_block."""
+    if stripe == 0:
+        return row_block(height, world, rank)
+    if world < 1 or not 0 <= rank < world or stripe & (stripe - 1):
+        raise ValueError(f"bad rank {rank} of {world} / stripe {stripe}")
+    total = -(-height // stripe)
+    count = (total - 1 - rank) // world + 1 if total > rank else 0
+    rows = count * stripe
+    if count and (total - 1 - rank) % world == 0 and height % stripe:
+        rows -= stripe - height % stripe
+    return rank * stripe, rows
+
+
+def frame_rows(height: int, world: int, rank: int, stripe: int = 0) -> list[int]:
+    """The frame rows of `rank`'s local rows 0, 1, ... (row_map.h: y_first + ly + (ly // stripe) * (period - stripe))."""
+    y0, rows = row_stripes(height, world, rank, stripe)
+    if stripe == 0:
+        return list(range(y0, y0 + rows))
+    gap = world * stripe - stripe
+    return [y0 + ly + (ly // stripe) * gap for ly in range(rows)]
+
+
 def pack_rgb(block):
     """The RGB channels of a [rows, W, 4] block as a contiguous [rows, W, 3] tensor (alpha is always 1.0)."""
     return block[..., :3].contiguous()

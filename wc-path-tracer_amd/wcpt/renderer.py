@@ -11,7 +11,8 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, GROUP_TRANSPORT_RCCL, GROUP_UNIQUE_ID_BYTES, OPTION_DIAGNOSTICS,
+from ._lib import (COUNTER_FIELDS, DRAW_COMMAND_DTYPE, GROUP_OPTION_ROW_STRIPE, GROUP_TRANSPORT_RCCL,
+                   GROUP_UNIQUE_ID_BYTES, OPTION_DIAGNOSTICS,
                    MATERIAL_DTYPE, SCENE_DATA_DTYPE, SPHERE_DTYPE, Camera, Counters, GroupInfo, WcptError, check, lib, ptr)
 from . import scene as _scene
 
@@ -117,6 +118,11 @@ class Context:
 
     def set_row_range(self, y0: int, rows: int):
         self._chk(lib.wcpt_set_row_range(self.h, y0, rows))
+
+    def set_row_stripes(self, y_first: int, rows: int, stripe: int, period: int):
+        """Interleaved stripes (wcpt_set_row_stripes): `rows` rows, stripes of `stripe` rows every `period` rows from
+        frame row y_first, stored back to back."""
+        self._chk(lib.wcpt_set_row_stripes(self.h, y_first, rows, stripe, period))
 
     def set_external_image(self, device_ptr: int, nbytes: int):
         self._chk(lib.wcpt_set_external_image(self.h, device_ptr, nbytes))
@@ -283,6 +289,10 @@ class Group:
 
     def set_option(self, option: int, value: int):
         check(lib.wcpt_group_set_option(self.h, option, value))
+        if option == GROUP_OPTION_ROW_STRIPE:
+            self.stripe = value
+            if getattr(self, "width", None):
+                self._set_rows()
 
     def info(self) -> dict:
         out = GroupInfo()
@@ -290,11 +300,14 @@ class Group:
         return out.as_dict()
 
     def create_screen(self, width: int, height: int):
-        from .dist import row_block
         check(lib.wcpt_group_create_screen(self.h, width, height))
         self.width, self.height = width, height
-        for r, c in self._ctx.items():   # a rank's context holds only its row block
-            c.width, c.height = width, row_block(height, self.nranks, r)[1]
+        self._set_rows()
+
+    def _set_rows(self):
+        from .dist import row_stripes
+        for r, c in self._ctx.items():   # a rank's context holds only its rows (a block, or interleaved stripes)
+            c.width, c.height = self.width, row_stripes(self.height, self.nranks, r, getattr(self, "stripe", 0))[1]
 
     def set_output(self, fmt: int, dst: int, nbytes: int):
         check(lib.wcpt_group_set_output(self.h, fmt, dst, nbytes))
