@@ -689,7 +689,7 @@ def test_context_row_stripes_and_frame_row_output(gpu_ctx, kernel):
     s = get_scene("cornell")
     W, H = 40, 52
     ref = _context_frames(s, W, H, (0, 1), kernel=kernel)
-    for y_first, rows, stripe, period in ((3, 20, 4, 12), (0, 13, 8, 16), (5, 47, 1, 1), (8, 24, 8, 24)):
+    for y_first, rows, stripe, period in ((3, 16, 4, 12), (0, 13, 8, 16), (5, 47, 1, 1), (8, 16, 8, 24)):
         with wcpt.Context(0) as ctx:
             dev = wcpt.DeviceScene(ctx, s)
             ctx.set_kernel(kernel)

@@ -698,6 +698,60 @@ __device__ __forceinline__ PairHit rayTrianglePairP(const Ray& r, const TriPairP
 #endif
     return h;
 }
+/* Exact sign pre-reject of a primary pair (WCPT_PRIM_SIGN_SKIP, VERDICT r05 item 3: execute fewer triangle tests).
+ * The reference's t is RN(tn * RN(1 / det)) (:126, :130), and a take needs t > 0 (:132). The primary records hold tn
+ * itself (tq, bit-identical to the test's), and det is the test's first result, so before the rest of the test: when
+ * the sign bits of tq and det differ, t is negative, -0 (an underflow) or NaN (a NaN operand) -- never > 0 -- and when
+ * det is +-0 or tq is +-0 with different signs the same holds (t = -inf, -0 or NaN). Such a triangle cannot be taken,
+ * whatever rec.t is. A wave whose every lane has both triangles of a pair in that case skips the pair's remaining
+ * operations (reciprocal, u, v, t, acceptance: 39 of its 53 VALU); a lane that may take either runs the whole test,
+ * so every result is the reference's. On primary rays (all from the camera, directions within one 8x8 tile) the sign
+ * of det -- which side of the triangle's plane the ray heads to -- is nearly uniform across a wave: on Cornell ~21 %
+ * of the primary pair steps are skippable by the whole wave (tools/prereject_sim.py; under 3 % on bounce rays, whose
+ * directions are random per lane, where the test therefore is not made). */
+#ifndef WCPT_PRIM_SIGN_SKIP
+#define WCPT_PRIM_SIGN_SKIP 1
+#endif
+__device__ __forceinline__ v2f pairP_det(const Ray& r, const TriPairP& p, v2f& px, v2f& py, v2f& pz)
+{
+    const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
+    px = dy * p.e2z - p.e2y * dz;
+    py = dz * p.e2x - p.e2z * dx;
+    pz = dx * p.e2y - p.e2x * dy;
+    return (p.e1x * px + p.e1y * py) + p.e1z * pz;
+}
+/* the rest of rayTrianglePairP after det (the same operations in the same order) */
+__device__ __forceinline__ PairHit pairP_finish(const Ray& r, const TriPairP& p, v2f px, v2f py, v2f pz, v2f det)
+{
+    const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
+    const v2f inv = rcp2_exact(det);
+    const v2f u = ((p.oax * px + p.oay * py) + p.oaz * pz) * inv;
+    const v2f v = (dx * (p.qx * inv) + dy * (p.qy * inv)) + dz * (p.qz * inv);
+    const v2f t = p.tq * inv;
+    const v2f uv = u + v;
+    PairHit h;
+    h.t = t;
+#if WCPT_PAIR_ITAKE
+    const v2f w = bc2(1.0f) - uv;
+    h.hit0 = accept_uvw(u.x, v.x, w.x);
+    h.hit1 = accept_uvw(u.y, v.y, w.y);
+#elif WCPT_ACCEPT_MIN3
+    const v2f w = bc2(1.0f) - uv;
+    h.hit0 = accept_tri_w(t.x, u.x, v.x, w.x);
+    h.hit1 = accept_tri_w(t.y, u.y, v.y, w.y);
+#else
+    h.hit0 = accept_tri(t.x, u.x, v.x, uv.x);
+    h.hit1 = accept_tri(t.y, u.y, v.y, uv.y);
+#endif
+    return h;
+}
+/* whether a lane may take either triangle of the pair: the sign bits of tq and det agree for at least one of them */
+__device__ __forceinline__ bool pairP_may_take(const TriPairP& p, v2f det)
+{
+    return (int32_t)(__float_as_uint(det.x) ^ __float_as_uint(p.tq.x)) >= 0 ||
+           (int32_t)(__float_as_uint(det.y) ^ __float_as_uint(p.tq.y)) >= 0;
+}
+
 /* The origin terms of one triangle (half h of pair record q) for origin o: build_primary_pairs */
 __device__ __forceinline__ void primary_terms(float ox, float oy, float oz, float ax, float ay, float az, float e1x,
                                               float e1y, float e1z, float e2x, float e2y, float e2z, float out[7])
@@ -1246,8 +1300,26 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
              * in the flat traversal loop it is correct (tools/stack_probe.py) */
             for (uint32_t o = offU; o < endU; o += kBytes) {
                 PairHit ph;
+#if WCPT_PRIM_SIGN_SKIP
+                if constexpr (PRIM) {
+                    const TriPairP p = load_pairP_const(pbase, o);
+                    v2f px, py, pz;
+                    const v2f det = pairP_det(ray, p, px, py, pz);
+                    if (__builtin_amdgcn_ballot_w64(pairP_may_take(p, det)) == 0ull) {
+                        /* no lane can take either triangle (t <= 0 or NaN for all): the reference's tests still
+                         * ran (and are counted), and none would change rec.t */
+                        count_tri<COUNT, DIAG>(cnt);
+                        count_tri<COUNT, DIAG>(cnt);
+                        continue;
+                    }
+                    ph = pairP_finish(ray, p, px, py, pz, det);
+                } else {
+                    ph = rayTrianglePair(ray, load_pair_const(pbase, o));
+                }
+#else
                 if constexpr (PRIM) ph = rayTrianglePairP(ray, load_pairP_const(pbase, o));
                 else ph = rayTrianglePair(ray, load_pair_const(pbase, o));
+#endif
 #if WCPT_DUP_PAIR
                 {
                     Ray r2 = ray;
