@@ -173,6 +173,7 @@ def test_bench_one_process_per_gpu_plumbing(tmp_path, world, one_visible):
     assert d["n_gpus"] == world and d["ranks"] == world and d["steps"] == 3
     assert d["group"]["transport"] == "rccl" and d["group"]["rccl_ranks"] == world
     assert d["group"]["kind"].startswith("one process per GPU")
+    assert d["launch"].startswith("external launcher")          # torchrun's environment, not bench.py's spawner
     assert "torch not imported" in d["hip_runtime"]
     # per-rank render times gathered in rank order (the stand-in's rank r takes 0.1 * (1 + r) ms per render); the
     # roofline's kernel time is the slowest rank's
