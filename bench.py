@@ -7,16 +7,22 @@ over RCCL). Rays = ray segments = Intersect() calls, counted exactly by the inst
 that were timed (untimed re-run).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|ref] [--camera still|orbit]
-                    [--transport rccl|copy] [--devices 0,1,..] [--verify] [--no-cpu-baseline]
+                    [--row-stripe S] [--one-process] [--transport rccl|copy|direct] [--devices 0,1,..] [--verify]
+                    [--rccl-rehearsal] [--no-cpu-baseline]
 
-Prints one JSON line on rank 0. Every mode drives the product's C ABI (include/wcpt.h wcpt_group_*) on the system HIP
-runtime (/opt/rocm), as the Jai host would; torch is not imported:
-  - no WORLD_SIZE (plain `python bench.py --gpus N`): one process, one host thread, a group over devices 0..N-1
-    (wcpt_group_create_ex; RCCL ncclCommInitAll, or --transport copy). --gpus 1 is a group of one, which renders
-    exactly as a single context.
-  - under torchrun (WORLD_SIZE = N): one process per GPU, rank RANK on device LOCAL_RANK (wcpt_group_create_rank,
-    ncclCommInitRank); the 128-byte RCCL id, barriers and the max-over-ranks time go through a TCP rendezvous
-    (wcpt.rdzv, MASTER_ADDR:MASTER_PORT+1). --gpus, if given, must equal WORLD_SIZE.
+Prints one JSON line on rank 0 (its "launch" field names how the ranks were started). Every mode drives the
+product's C ABI (include/wcpt.h wcpt_group_*) on the system HIP runtime (/opt/rocm), as the Jai host would; torch is
+not imported:
+  - --gpus 1 (the default): a group of one, which renders exactly as a single context.
+  - under a launcher (torchrun: WORLD_SIZE = N): this process is rank RANK of a one-process-per-GPU group on device
+    LOCAL_RANK (wcpt_group_create_rank, ncclCommInitRank); the 128-byte RCCL id, barriers and the max-over-ranks time
+    go through a TCP rendezvous (wcpt.rdzv, MASTER_ADDR:MASTER_PORT+1). --gpus, if given, must equal WORLD_SIZE.
+  - plain `python bench.py --gpus N` (N > 1, no launcher): before anything touches a GPU, this process spawns N fresh
+    rank processes with torchrun's environment (spawn_ranks; never an exec) and waits for them: the same
+    one-process-per-GPU path as under torchrun.
+  - --one-process (or --transport copy|direct, or --devices): one process, one host thread, a group over devices
+    0..N-1 (wcpt_group_create_ex; RCCL ncclCommInitAll, or the COPY / DIRECT transports). Its RCCL form over several
+    GPUs has never run on hardware, and its line says "unrehearsed".
   - --dist-backend gloo | gloo-host | torch-nccl under torchrun: the torch.distributed gather of rounds 1-3 (torch
     imported first, so libwcpt binds torch's bundled HIP runtime): N-rank rehearsals on one GPU.
 """
@@ -398,8 +404,8 @@ def parse_args(argv=None):
                          "render (WCPT_GROUP_OPTION_OVERLAP 0)")
     ap.add_argument("--group-threads", type=int, default=None, choices=[-1, 0, 1],
                     help="one-process group: issue each rank's share of a frame from a host thread of its own "
-                         "(WCPT_GROUP_OPTION_THREADS; default: the library's, -1 = on when the ranks span several "
-                         "devices)")
+                         "(WCPT_GROUP_OPTION_THREADS; default: the library's, 0 = off; -1 = on when the ranks span "
+                         "several devices)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "copy", "direct"],
                     help="one-process group: RCCL send/recv (default), hipMemcpyPeerAsync of each block, or direct: "
                          "each rank's render writes its rows of the root's frame over xGMI (no transfer step)")
@@ -537,7 +543,7 @@ def resolve_topology(args, env) -> dict:
     if args.dist_backend != "rccl":
         raise SystemExit(f"bench.py: --dist-backend {args.dist_backend} needs a torchrun launch (WORLD_SIZE > 1)")
     if args.rccl_rehearsal:
-        raise SystemExit("bench.py: --rccl-rehearsal needs a torchrun launch (WORLD_SIZE > 1)")
+        raise SystemExit("bench.py: --rccl-rehearsal needs several ranks (--gpus N > 1, or a launcher's WORLD_SIZE)")
     n = 1 if args.gpus is None else args.gpus
     if n < 1:
         raise SystemExit(f"bench.py: --gpus {n}")
