@@ -95,7 +95,10 @@ extern "C" {
 #define WCPT_OPTION_PACKED_REFS 7
 /* Wavefront trace: a wave fetches new rays once this many of its 64 lanes are idle (1..64, default 20: fewer,
  * fuller fetch rounds; c3 9.0 -> 8.2 ms at 12 against 1; round 5, with the finished lanes' hit records stored at the
- * refill: c4 197.8-198.2 ms at 20 against 199.5 at 12 and 201.3 at 32, c3 unchanged within the spread). */
+ * refill: c4 197.8-198.2 ms at 20 against 199.5 at 12 and 201.3 at 32, c3 unchanged within the spread). The
+ * path-persistent trace (WCPT_OPTION_WF_PERSIST) reads it as its fetch and shading-batch threshold too, with its own
+ * default of 12 while the option is unset (round 6: c3 8-way shares 1 % faster than at 20); a value set here governs
+ * both. */
 #define WCPT_OPTION_WF_REFILL 8
 /* Megakernel tile order: 0 each XCD walks a contiguous band of 8x8 tiles; 1 scattered (tile b * m mod tiles), so the
  * tiles resident on a CU at once come from all over the frame; 3, 4, 5, 6 XCD bands striped by 1, 2, 4, 8 tile rows

@@ -29,6 +29,7 @@ struct LaunchArgs {
     const uint64_t* tri_records; /* device table [drawCommandCount] of {singles, pairs, triangle count, -} */
     bool pair_records;           /* megakernel: leaf tests on pair records (fat leaves) instead of singles */
     uint32_t wf_refill;          /* wavefront trace: idle lanes that trigger a ray fetch (1..64) */
+    uint32_t wf_refill_persist;  /* the path-persistent trace's refill and shading-batch threshold (1..64) */
     int wf_fetch;                /* wavefront trace fetch rounds per iteration: -1 auto, 0 two, 1 one (WCPT_OPTION_WF_FETCH) */
     int wf_persist;              /* path-persistent trace: -1 auto, 0 off, 1 wherever eligible (WCPT_OPTION_WF_PERSIST) */
     bool wf_fast;                /* wavefront trace: draw 0 has packed stack refs, 24-bit record offsets, leaves of < 255

@@ -952,7 +952,8 @@ static hipError_t wf_persist_variant(bool query, int& bpc, const LaunchArgs& a, 
     if (query)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::wf_trace<false, false, GEO, 10, true>, 64, 0);
     hipLaunchKernelGGL((dev::wf_trace<false, false, GEO, 10, true>), dim3(grid), dim3(64), 0, stream, a.sd, a.draws,
-                       a.tri_records, b, a.status, a.counters, a.wf_refill, a.materials, a.spheres, a.image, a.W, a.H);
+                       a.tri_records, b, a.status, a.counters, a.wf_refill_persist, a.materials, a.spheres, a.image, a.W,
+                       a.H);
     return hipGetLastError();
 }
 static hipError_t wf_persist_dispatch(int geo, bool query, int& bpc, const LaunchArgs& a, const WfBuffers& b,

@@ -157,6 +157,10 @@ struct wcpt_context {
     int wf_fetch = -1;                 /* WCPT_OPTION_WF_FETCH */
     int wf_persist = -1;               /* WCPT_OPTION_WF_PERSIST */
     int wf_refill = 20;                /* WCPT_OPTION_WF_REFILL (round 5 with the deferred hit stores, c4: 8 / 12 / 16 / 20 / 24 / 32 -> 203.5 / 199.6 / 198.9 / 198.0 / 198.6 / 201.4 ms; c3 flat; profiles/r05_fetch_once_ab.log) */
+    /* the path-persistent trace's threshold while the option is unset (round 6, c3 8-way slowest share over 3 rounds,
+     * refill 8 / 12 / 16 / 20: 8-row stripes 1.265 / 1.250 / 1.249 / 1.262 ms, row blocks 1.314 / 1.280 / 1.293 / 1.287
+     * ms; profiles/r06_persist_refill_sweep_c3.log) */
+    int wf_refill_persist = 12;
 #ifndef WCPT_WF_PIPES_DEFAULT
 #define WCPT_WF_PIPES_DEFAULT 0
 #endif
@@ -572,6 +576,7 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
     a.pair_records = false;
     a.wf_fast = false;
     a.wf_refill = (uint32_t)ctx->wf_refill;
+    a.wf_refill_persist = (uint32_t)ctx->wf_refill_persist;
     a.wf_fetch = ctx->wf_fetch;
     a.wf_persist = ctx->wf_persist;
     a.mk_tile_order = (uint32_t)ctx->mk_tile_order;
@@ -883,6 +888,7 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     case WCPT_OPTION_WF_REFILL:
         if (value < 1 || value > 64) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "refill threshold %d", value);
         ctx->wf_refill = value;
+        ctx->wf_refill_persist = value; /* an explicit value governs both traces */
         return WCPT_SUCCESS;
     case WCPT_OPTION_WF_PIPES:
         if (value < 0 || value > wcpt::kWfMaxPipes) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "pipelines %d", value);
