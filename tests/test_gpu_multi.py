@@ -734,3 +734,42 @@ def test_row_stripe_errors(gpu_ctx):
         assert [c.height for c in g.contexts] == [8, 8, 1]
         assert g.info()["broken"] == 0
     del s
+
+
+# ---- the one-process-per-GPU RCCL path, spawned by bench.py, and its bounded sync (round 6) ------------------------------
+def _run(cmd, timeout):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable] + cmd, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                          env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_spawned_rccl_ranks_present_the_one_device_frame(gpu_ctx):
+    """`python bench.py --gpus 2 --rccl-rehearsal --verify` with no launcher: bench.py spawns two rank processes, each
+    runs wcpt_group_create_rank (ncclCommInitRank) and the planned ncclSend / ncclRecv of every frame over RCCL's socket
+    transport (a NCCL_HOSTID per rank lets two ranks share the one GPU), with interleaved 8-row stripes (the root's
+    staging buffer and 2D scatter); the presented frame equals one device's render bit for bit."""
+    import json
+    p = _run(["bench.py", "--gpus", "2", "--config", "c1", "--rccl-rehearsal", "--row-stripe", "8", "--verify",
+              "--steps", "6", "--warmup", "2", "--settle-ms", "0", "--no-cpu-baseline", "--watchdog-s", "100"], 150)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["verified"] is True and d["ranks"] == 2 and d["group"]["rccl_ranks"] == 2
+    assert d["launch"].startswith("spawned by bench.py")
+
+
+def test_group_sync_returns_device_lost_when_a_peer_skips_a_frame(gpu_ctx):
+    """VERDICT r05 item 2 on the GPU (tools/group_fault_probe.py): rank 1 skips one frame's wcpt_group_render, so the
+    root's receive never completes; its wcpt_group_sync returns WCPT_ERROR_DEVICE_LOST at the 2-s
+    WCPT_GROUP_OPTION_TIMEOUT_MS (communicator aborted, the next render refused) instead of hanging, and both processes
+    destroy their groups and exit."""
+    import json
+    p = _run(["tools/group_fault_probe.py", "--ranks", "2", "--timeout-ms", "2000"], 150)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["ok"] and all(d["checks"].values()), d["checks"]
+    assert d["per_rank"][0]["sync_frame_3"]["rc"] == "WCPT_ERROR_DEVICE_LOST"
