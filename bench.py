@@ -487,15 +487,31 @@ def spawn_ranks(argv, n: int, env=None, child_cmd=None, timeout_s: float = 0.0, 
     terminated (they would wait for its exchange); returns 0, the first failing rank's exit status (128 + signal for a
     signalled one), or 3 when the ranks outlive `timeout_s`."""
     import secrets
+    import signal
     import subprocess
     env = dict(os.environ if env is None else env)
     cmd = list(child_cmd) if child_cmd else [sys.executable, os.path.abspath(__file__)]
     port = _free_tcp_port()
     run_id = f"wcpt-spawn-{os.getpid()}-{secrets.token_hex(4)}"
     procs = []
+
+    def die_with_parent():
+        # in the child before it runs the rank: a SIGKILL when this spawner dies, so no rank outlives it holding a GPU
+        # (Linux prctl PR_SET_PDEATHSIG; the spawner has made no HIP call, so forking it is safe)
+        try:
+            import ctypes
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGKILL)
+        except (OSError, AttributeError):
+            pass
+
+    def on_term(signum, frame):   # a launcher's SIGTERM / SIGINT: stop the ranks (the finally below), then exit
+        raise SystemExit(128 + signum)
+
+    old = {sig: signal.signal(sig, on_term) for sig in (signal.SIGTERM, signal.SIGINT)}
     try:
         for r in range(n):
-            procs.append(subprocess.Popen(cmd + list(argv), env=spawn_env(env, n, r, port, run_id)))
+            procs.append(subprocess.Popen(cmd + list(argv), env=spawn_env(env, n, r, port, run_id),
+                                          preexec_fn=die_with_parent))
         deadline = time.monotonic() + timeout_s if timeout_s and timeout_s > 0 else None
         rc = 0
         while [p.poll() for p in procs].count(None):      # poll every rank (any() would stop at the first)
@@ -521,6 +537,8 @@ def spawn_ranks(argv, n: int, env=None, child_cmd=None, timeout_s: float = 0.0, 
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+        for sig, h in old.items():
+            signal.signal(sig, h)
     return 128 - rc if rc < 0 else rc
 
 

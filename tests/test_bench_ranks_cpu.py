@@ -281,3 +281,39 @@ def test_a_failing_rank_stops_the_others(tmp_path, capfd):
     err = capfd.readouterr().err
     assert rc == 7 and dt < 60
     assert "rank 1 exited with 7" in err
+
+
+@pytest.mark.parametrize("how", ["sigterm", "sigkill"])
+def test_spawner_sigterm_stops_the_ranks(tmp_path, how):
+    """A launcher's SIGTERM to the spawner (or its death) must not leave rank processes holding GPUs: the spawner stops
+    its ranks on SIGTERM and exits 128 + 15; each rank also has PR_SET_PDEATHSIG, so it dies with the spawner."""
+    import signal
+    import subprocess
+    pid_dir = tmp_path / "pids"
+    pid_dir.mkdir()
+    rank = tmp_path / "rank.py"
+    rank.write_text("import os, sys, time\nopen(os.path.join(sys.argv[1], str(os.getpid())), 'w').close()\n"
+                    "time.sleep(300)\n")
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.spawn_ranks([%r], 2, child_cmd=[sys.executable, %r]))") % (ROOT, str(pid_dir), str(rank))
+    p = subprocess.Popen([sys.executable, "-c", code])
+    t0 = time.monotonic()
+    while len(os.listdir(pid_dir)) < 2 and time.monotonic() - t0 < 30:
+        time.sleep(0.05)
+    pids = [int(x) for x in os.listdir(pid_dir)]
+    assert len(pids) == 2
+    if how == "sigterm":
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    else:                      # the spawner dies without a word: PR_SET_PDEATHSIG takes its ranks with it
+        p.kill()
+        p.wait(timeout=30)
+    for pid in pids:
+        for _ in range(200):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.05)
+        else:
+            raise AssertionError(f"rank {pid} still running")
