@@ -712,6 +712,9 @@ __device__ __forceinline__ PairHit rayTrianglePairP(const Ray& r, const TriPairP
 #ifndef WCPT_PRIM_SIGN_SKIP
 #define WCPT_PRIM_SIGN_SKIP 1
 #endif
+#ifndef WCPT_PAIR_PREFETCH
+#define WCPT_PAIR_PREFETCH 0
+#endif
 __device__ __forceinline__ v2f pairP_det(const Ray& r, const TriPairP& p, v2f& px, v2f& py, v2f& pz)
 {
     const v2f dx = bc2(r.direction.x), dy = bc2(r.direction.y), dz = bc2(r.direction.z);
@@ -1298,6 +1301,27 @@ __device__ __forceinline__ void pair_leaf(const Ray& ray, gtri_ptr recs, uint32_
             /* the loop counter itself in an SGPR (offU..endU): no per-lane offset arithmetic (70 -> 68 VALU per
              * pair, c2 -1.7 %). A wave-uniform loop like this one was mis-compiled inside the old nested draw loop;
              * in the flat traversal loop it is correct (tools/stack_probe.py) */
+#if WCPT_PAIR_PREFETCH
+            if constexpr (!PRIM) {
+                /* software-pipelined scalar records: the next pair's record is requested before this pair is tested,
+                 * so its scalar-cache latency hides behind the test. The record one past the leaf's whole pairs is
+                 * inside the draw's allocation (runtime: ntri / 2 + 1 pair records) and is never used. */
+                TriPair cur = load_pair_const(pbase, offU);
+                for (uint32_t o = offU; o < endU; o += kBytes) {
+                    const TriPair nxt = load_pair_const(pbase, o + kBytes);
+                    const PairHit ph = rayTrianglePair(ray, cur);
+                    count_tri<COUNT, DIAG>(cnt);
+                    count_tri<COUNT, DIAG>(cnt);
+#if WCPT_PAIR_ITAKE
+                    pair_take_bits(ph, o, rb, tag);
+#else
+                    pair_take(ph, o, rt, tag);
+#endif
+                    cur = nxt;
+                }
+                off = offEnd;
+            } else
+#endif
             for (uint32_t o = offU; o < endU; o += kBytes) {
                 PairHit ph;
 #if WCPT_PRIM_SIGN_SKIP

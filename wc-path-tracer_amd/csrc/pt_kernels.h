@@ -92,6 +92,10 @@ struct WfState {
     int cus = 0;                   /* compute units of the context's device (0 = not yet queried)          */
     int trace_bpc[3][3][3] = {};   /* trace-kernel blocks per CU by (mode, geometry variant, LDS stack)      */
     int persist_bpc = 0;           /* the path-persistent trace's blocks per CU                             */
+    /* queue counters: two sets of {count q0, count q1, trace head, -}; a frame uses set `parity` and its ray generation
+     * zeroes the other set for the next frame (pt_wavefront.hip WCPT_WF_CTR_PARITY); `ctr_fresh` until the first zeroing */
+    uint32_t parity = 0;
+    bool ctr_fresh = true;
 };
 
 /* Concurrent wavefront pipelines (WCPT_OPTION_WF_PIPES): pipeline j of K owns the 8x8 tiles t with t % K == j and

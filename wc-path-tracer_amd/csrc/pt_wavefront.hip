@@ -124,6 +124,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool pred, u
  * goes on with the path's next segment, so no path waits for the slowest ray of its bounce; the wave shades once
  * `refill` of its lanes wait, or when none is tracing. Used where a pipeline's queue is short (row blocks), for one
  * sample per pixel. */
+#ifndef WCPT_WF_CTR_PARITY
+#define WCPT_WF_CTR_PARITY 1
+#endif
 #ifndef WCPT_WF_PERSIST_WAVES
 #define WCPT_WF_PERSIST_WAVES 4
 #endif
@@ -140,8 +143,12 @@ __global__ __launch_bounds__(kShadeBlock) void wf_init(const wcpt_scene_data sd,
                                                        WfBuffers b, float4* __restrict__ image,
                                                        uint32_t W, uint32_t H, const RowMap rm, uint32_t rows,
                                                        uint32_t tilesX, uint32_t total, uint32_t pipe, uint32_t npipes,
-                                                       unsigned long long* __restrict__ counters)
+                                                       unsigned long long* __restrict__ counters,
+                                                       uint32_t* __restrict__ zero_next)
 {
+    /* the queue counters of the pipeline's next frame (the other counter set, unused by this frame): zeroed here, so a
+     * frame needs no memset launch of its own (WCPT_WF_CTR_PARITY) */
+    if (zero_next && blockIdx.x == 0 && threadIdx.x < 4u) zero_next[threadIdx.x] = 0u;
     __shared__ uint32_t s_wave[kShadeBlock / 64], s_base;
     Counters cnt = {};
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
@@ -810,8 +817,10 @@ hipError_t wf_reserve(WfState& s, uint32_t paths)
         s.soa[k].pix = u + P;
         u += 2 * P;
     }
-    s.ctr = u; /* [0] count q0, [1] count q1, [2] trace head */
-    s.diag = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(s.ctr + 4 + 7) & ~uintptr_t(7));
+    s.ctr = u; /* two sets of [0] count q0, [1] count q1, [2] trace head, [3] - (WCPT_WF_CTR_PARITY) */
+    s.diag = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(s.ctr + 8 + 7) & ~uintptr_t(7));
+    s.parity = 0;
+    s.ctr_fresh = true;
     s.capacity = paths; /* only now: every array above exists */
     return hipSuccess;
 }
@@ -1033,15 +1042,34 @@ static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const Wf
     hipError_t e = wf_reserve(s, P);
     if (e != hipSuccess) return e;
     const bool count = mode != kModeRender;
+    /* The queue counters must start at zero. WCPT_WF_CTR_PARITY: the pipeline alternates between two counter sets,
+     * and each frame's wf_init zeroes the set the next frame uses -- the frames of one pipeline run in order on its
+     * stream (and a render's pipelines join before the next render forks), so the previous frame, the only other user
+     * of that set, has finished; only a fresh allocation is zeroed with a memset. Otherwise one memset per pipeline
+     * and frame (a fill kernel launch in the pipeline's chain). */
+    uint32_t* ctr = s.ctr;
+    uint32_t* zero_next = nullptr;
+#if WCPT_WF_CTR_PARITY
+    if (s.ctr_fresh) {
+        e = hipMemsetAsync(s.ctr, 0, 8 * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        s.ctr_fresh = false;
+        s.parity = 0;
+    }
+    ctr = s.ctr + 4u * s.parity;
+    zero_next = s.ctr + 4u * (s.parity ^ 1u);
+    s.parity ^= 1u;
+#else
     e = hipMemsetAsync(s.ctr, 0, 4 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+#endif
     b.in = s.soa[0];
     b.out = s.soa[1];
     b.result = result;
     b.prim_hit = prim_hit;
     b.hit = s.hit;
     b.order = nullptr;
-    b.head = s.ctr + 2;
+    b.head = ctr + 2;
     b.diag = s0.diag;
     if (mode == kModeDiag) {
         e = hipMemsetAsync(s0.diag, 0, dev::kDiagTimers * sizeof(unsigned long long), stream);
@@ -1050,15 +1078,17 @@ static hipError_t pipe_begin(const LaunchArgs& a, int mode, WfState& s, const Wf
     b.wire = a.wire;
     b.wire_ch = a.wire_ch;
     b.wire_rows = a.wire_rows;
-    b.count_in = s.ctr + 0;
-    b.count_out = s.ctr + 1;
+    b.count_in = ctr + 0;
+    b.count_out = ctr + 1;
     const uint32_t init_grid = min((total + dev::kShadeBlock - 1) / dev::kShadeBlock, (uint32_t)cus * 16u);
     if (count)
         hipLaunchKernelGGL(dev::wf_init<true>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
-                           a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.rows, tilesX, total, pipe, npipes, a.counters);
+                           a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.rows, tilesX, total, pipe, npipes, a.counters,
+                           zero_next);
     else
         hipLaunchKernelGGL(dev::wf_init<false>, dim3(init_grid), dim3(dev::kShadeBlock), 0, stream, a.sd, a.spheres, b, a.image,
-                           a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.rows, tilesX, total, pipe, npipes, a.counters);
+                           a.W, a.H, RowMap{a.y0, a.row_shift, a.row_gap}, a.rows, tilesX, total, pipe, npipes, a.counters,
+                           zero_next);
     return hipGetLastError();
 }
 
