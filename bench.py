@@ -380,6 +380,8 @@ def parse_args(argv=None):
                     help="WCPT_OPTION_WF_FETCH: wavefront trace fetch rounds per iteration (-1: the library's choice)")
     ap.add_argument("--wf-persist", type=int, default=-1, choices=[-1, 0, 1],
                     help="WCPT_OPTION_WF_PERSIST: the path-persistent wavefront trace (-1: the library's choice)")
+    ap.add_argument("--frame-overlap", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="WCPT_OPTION_FRAME_OVERLAP: megakernel frames overlapped on two pipes (-1: the library's default)")
     ap.add_argument("--wf-pipes", type=int, default=0,
                     help="wavefront kernel: concurrent pipelines (WCPT_OPTION_WF_PIPES; 0 = the library default)")
     ap.add_argument("--camera", default="still", choices=["still", "orbit"],
@@ -649,6 +651,8 @@ class GroupBench:
                 c.set_option(T.OPTION_WF_FETCH, args.wf_fetch)
             if args.wf_persist >= 0:
                 c.set_option(T.OPTION_WF_PERSIST, args.wf_persist)
+            if getattr(args, "frame_overlap", -1) >= 0:
+                c.set_option(T.OPTION_FRAME_OVERLAP, args.frame_overlap)
             self.devs.append(wcpt.DeviceScene(c, scene))
         self.g.set_option(T.GROUP_OPTION_OVERLAP, 0 if args.no_overlap else 1)
         if getattr(args, "group_threads", None) is not None:
@@ -773,6 +777,8 @@ class TorchBench:
             self.ctx.set_option(wcpt._lib.OPTION_WF_FETCH, args.wf_fetch)
         if args.wf_persist >= 0:
             self.ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, args.wf_persist)
+        if getattr(args, "frame_overlap", -1) >= 0:
+            self.ctx.set_option(wcpt._lib.OPTION_FRAME_OVERLAP, args.frame_overlap)
         self.dev = wcpt.DeviceScene(self.ctx, scene)
         self.ctx.create_screen(W, H)
         y0, rows = row_block(H, self.world, self.rank)
@@ -1106,6 +1112,7 @@ def main(argv=None):
                        "camera": args.camera,
                        "kernel": {0: "megakernel", 2: "wavefront"}[args.kernel] +
                                  (" (WCPT_KERNEL_AUTO's choice)" if args.kernel_auto else ""), "bvh": args.bvh,
+                       "frame_overlap": {-1: "library default (auto)", 0: "off", 1: "auto", 2: "on"}[args.frame_overlap],
                        "parallelism": ((f"row-stripes of {args.row_stripe} rows x{nranks}" if args.row_stripe else
                                         f"row-block x{nranks}") + f" + {transport} gather of {args.gather} blocks"
                                        + ("" if args.no_overlap else " overlapped with the next frame")

@@ -133,6 +133,15 @@ extern "C" {
  * blocks or interleaved stripes alike); 0 (default) = the context's rows back to back (row ly of its rows at row ly).
  * Added under ABI 4. */
 #define WCPT_OPTION_GATHER_FRAME_ROWS 14
+/* Frame overlap (megakernel, cost-ordered tiles): consecutive renders with no other call on the context between them
+ * run as two pipes, each on a stream of its own and owning half the tiles (the same pixels in every frame), so one
+ * pipe's next frame starts in the other's last round of waves instead of behind the whole frame. Every other entry
+ * point (wcpt_sync, readback, composite, profile end, buffer calls, a group's exchange ...) first orders the context's
+ * stream after both pipes, so what it sees or queues is as if each render had run on the stream; hence only on the
+ * context's own stream (not after wcpt_set_stream) and not under per-render timing events. 1 (default): from two rounds
+ * of resident waves up (a 1920x1080 frame, not an 8-way row block); 0 off; 2 whenever the tiles are cost-ordered.
+ * Same results. Added under ABI 4. */
+#define WCPT_OPTION_FRAME_OVERLAP 15
 
 /* ---- POD types with the reference byte layouts -------------------------------------------------- */
 

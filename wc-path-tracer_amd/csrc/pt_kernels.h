@@ -111,7 +111,13 @@ struct WfPipes {
     hipEvent_t fork = nullptr;
     hipEvent_t join[kWfMaxPipes] = {};
     hipEvent_t ready[kWfMaxPipes] = {};  /* pipeline j's init has run (WCPT_WF_START_TOGETHER) */
+    /* frame overlap (WCPT_OPTION_FRAME_OVERLAP): pipelines 1..pending_pipes-1 hold frames the context's stream has not
+     * been joined to (wf_join), of a frame of pending_W x pending_rows */
+    bool pending = false;
+    uint32_t pending_pipes = 0, pending_W = 0, pending_rows = 0;
+    bool pending_persist = false;
 };
+hipError_t wf_join(WfPipes& w, hipStream_t stream);
 
 /* Megakernel launch state, per context. */
 struct MkState {
@@ -131,8 +137,26 @@ struct MkState {
     uint32_t geom_shift = kContiguousShift, geom_gap = 0;            /* ... and its frame rows (row_map.h) */
     uint32_t renders = 0;      /* renders of that geometry */
     bool order_valid = false;
+    /* Frame overlap (WCPT_OPTION_FRAME_OVERLAP, pt_kernels.hip launch_megakernel): a render splits the cost-ordered
+     * tiles between two pipes (tile list `split`: the order's even positions, then its odd ones), pipe 0 on the
+     * context's stream and pipe 1 on a stream of its own, and the next render's pipes continue without waiting for the
+     * other pipe -- each pipe owns the same pixels in every frame, so per pixel the frames stay in order. `pending`: frames on the pipe streams that the
+     * context's stream has not been joined to (mk_join; every entry point other than a render joins first). */
+    uint32_t* split = nullptr; /* `cap` u32 after `order` */
+    bool split_valid = false;
+    bool pending = false;
+    uint32_t pending_tiles = 0;
+    hipStream_t pipe[2] = {};  /* [1]: pipe 1's stream (pipe 0 runs on the context's stream) */
+    hipEvent_t fork = nullptr;
+    hipEvent_t join[2] = {};
 };
+constexpr uint32_t kMkPipes = 2;
 void mk_release(MkState& mk);
+/* The context's stream continues after every frame the overlap pipes hold (no-op when none is pending). */
+/* A group suppresses the overlap on a context whose frames it joins every frame anyway (a sender's ready event, the
+ * root's in-line receives): there a fork and a join per frame would cost more than the tail they hide. */
+void set_overlap_suppressed(wcpt_context* ctx, bool on);
+hipError_t mk_join(MkState& mk, hipStream_t stream);
 
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD
  * diagnostics (ballot-based step counters, tools/diag.py). */
@@ -160,12 +184,15 @@ hipError_t launch_build_tri_records(const uint32_t* indices, const float* vertic
                                     uint32_t vertex_count, void* singles, void* pairs, hipStream_t stream);
 /* composite.comp (pt_composite.hip): gamma + PBR Neutral over `pixels` float4 texels into rgba32f or RGBA8 */
 hipError_t launch_composite(const float4* img, uint64_t pixels, void* dst, bool rgba8, int cus, hipStream_t stream);
-hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream);
+/* overlap: WCPT_OPTION_FRAME_OVERLAP as the runtime allows it for this render (0 off, 1 auto, 2 on whenever the tiles
+ * are cost-ordered); with 0 a pending overlap is joined first and the frame runs on `stream` */
+hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream,
+                             int overlap = 0);
 /* sort_rays: sort the ray queue by (direction octant, origin Morton code) before each bounce's trace. */
 /* lds_stack: LDS traversal-stack entries per lane of the trace kernel (10, 16 or 24; render mode only). */
 /* pipes: concurrent pipelines (1..kWfMaxPipes; sorting and diagnostics use 1). */
 hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes, bool sort_rays, int lds_stack,
-                            hipStream_t stream);
+                            hipStream_t stream, int overlap = 0);
 hipError_t wf_reserve(WfState& s, uint32_t paths);
 hipError_t wf_reserve_sort(WfState& s, uint32_t paths);
 void wf_release(WfState& s);

@@ -413,8 +413,11 @@ hipError_t launch_build_primary_pairs(const void* pairs, uint32_t npairs, float 
     return hipGetLastError();
 }
 
+/* list / grid: a frame-overlap pipe's share of the cost-ordered tiles (MkState::split); null: every tile, in the order
+ * below */
 template <bool COUNT, bool DIAG, int SK, bool PAIRS, bool SINGLE, bool REUSE = false>
-static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stream, uint32_t tilesX, uint32_t tiles)
+static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stream, uint32_t tilesX, uint32_t tiles,
+                              const uint32_t* list, uint32_t grid)
 {
     /* scattered tile order: block b renders tile (b * m) mod tiles for an m coprime with tiles near 0.618 * tiles,
      * so the tiles resident on one CU at once come from all over the frame */
@@ -434,9 +437,10 @@ static hipError_t launch_mega(const LaunchArgs& a, MkState& mk, hipStream_t stre
     /* cost-ordered tiles (auto order, render launches): this render records every tile's time, and the renders after
      * a sort (launch_megakernel) take the tiles longest first */
     const bool cost_order = !COUNT && a.mk_tile_order == 2 && mk.cost != nullptr;
-    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE, REUSE>), dim3(tiles), dim3(64), 0, stream, a.sd,
-                       a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H,
-                       RowMap{a.y0, a.row_shift, a.row_gap}, a.wire_rows, a.rows, tilesX, tiles, scatter, cost_order && mk.order_valid ? mk.order : nullptr,
+    const uint32_t* order = list ? list : (cost_order && mk.order_valid ? mk.order : nullptr);
+    hipLaunchKernelGGL((dev::pt_megakernel<COUNT, DIAG, SK, PAIRS, SINGLE, REUSE>), dim3(list ? grid : tiles), dim3(64), 0,
+                       stream, a.sd, a.materials, a.spheres, a.draws, a.tri_records, a.image, a.wire, a.wire_ch, a.W, a.H,
+                       RowMap{a.y0, a.row_shift, a.row_gap}, a.wire_rows, a.rows, tilesX, tiles, scatter, order,
                        cost_order ? mk.cost : nullptr, a.status, a.counters);
     return hipGetLastError();
 }
@@ -446,8 +450,21 @@ __global__ void fill_iota(uint32_t* __restrict__ v, uint32_t n)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = i;
 }
 
+__global__ void split_tiles(const uint32_t* __restrict__ order, uint32_t n, uint32_t* __restrict__ out)
+{
+    const uint32_t half = (n + 1u) / 2u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out[(i & 1u) ? half + (i >> 1) : (i >> 1)] = order[i];
+}
+
+/* the caller has synchronised the context's stream after mk_join */
 void mk_release(MkState& mk)
 {
+    for (uint32_t p = 0; p < kMkPipes; p++) {
+        if (mk.pipe[p]) (void)hipStreamDestroy(mk.pipe[p]);
+        if (mk.join[p]) (void)hipEventDestroy(mk.join[p]);
+    }
+    if (mk.fork) (void)hipEventDestroy(mk.fork);
     if (mk.mem) (void)hipFree(mk.mem);
     const int cus = mk.cus;
     mk = MkState{};
@@ -477,7 +494,7 @@ static hipError_t cost_order_prepare(const LaunchArgs& a, MkState& mk, uint32_t 
                                                                     (uint32_t*)nullptr, (const uint32_t*)nullptr,
                                                                     (uint32_t*)nullptr, (int)tiles, 0, 32, stream);
         if (e != hipSuccess) return e;
-        const size_t words = 4ull * tiles;
+        const size_t words = 5ull * tiles;
         const size_t bytes = ((words * 4ull + 255ull) & ~255ull) + temp;
         void* m = nullptr;
         e = hipMalloc(&m, bytes);
@@ -488,6 +505,7 @@ static hipError_t cost_order_prepare(const LaunchArgs& a, MkState& mk, uint32_t 
         mk.keys = u + tiles;
         mk.iota = u + 2ull * tiles;
         mk.order = u + 3ull * tiles;
+        mk.split = u + 4ull * tiles;
         mk.temp = static_cast<char*>(m) + ((words * 4ull + 255ull) & ~255ull);
         mk.temp_bytes = temp;
         mk.cap = tiles;
@@ -503,6 +521,7 @@ static hipError_t cost_order_prepare(const LaunchArgs& a, MkState& mk, uint32_t 
         mk.geom_gap = a.row_gap;
         mk.renders = 0;
         mk.order_valid = false;
+        mk.split_valid = false;
         return hipMemsetAsync(mk.cost, 0, (size_t)tiles * 4u, stream); /* the running averages start at 0 */
     }
     return hipSuccess;
@@ -517,36 +536,68 @@ static hipError_t cost_order_sort(MkState& mk, uint32_t tiles, hipStream_t strea
     size_t temp = mk.temp_bytes;
     e = hipcub::DeviceRadixSort::SortPairsDescending(mk.temp, temp, mk.cost, mk.keys, mk.iota, mk.order, (int)tiles, 0,
                                                      32, stream);
-    if (e == hipSuccess) mk.order_valid = true;
+    if (e != hipSuccess) return e;
+    mk.order_valid = true;
+    /* the frame-overlap pipes' tile lists: the order's even positions, then its odd ones (each list longest first) */
+    hipLaunchKernelGGL(split_tiles, dim3(std::min<uint32_t>((tiles + 255u) / 256u, 1024u)), dim3(256), 0, stream,
+                       mk.order, tiles, mk.split);
+    e = hipGetLastError();
+    mk.split_valid = e == hipSuccess;
     return e;
 }
 
 template <bool PAIRS, bool SINGLE>
 static hipError_t launch_mega_sk(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream,
-                                 uint32_t tilesX, uint32_t tiles)
+                                 uint32_t tilesX, uint32_t tiles, const uint32_t* list = nullptr, uint32_t grid = 0)
 {
     if (stack_kind == 0) {
         if (mode == kModeRender)
             return a.sd.samples > 1u && WCPT_MK_PRIMARY_REUSE
-                       ? launch_mega<false, false, 0, PAIRS, SINGLE, true>(a, mk, stream, tilesX, tiles)
-                       : launch_mega<false, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
-        if (mode == kModeCount) return launch_mega<true, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
-        return launch_mega<true, true, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+                       ? launch_mega<false, false, 0, PAIRS, SINGLE, true>(a, mk, stream, tilesX, tiles, list, grid)
+                       : launch_mega<false, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles, list, grid);
+        if (mode == kModeCount) return launch_mega<true, false, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles, list, grid);
+        return launch_mega<true, true, 0, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles, list, grid);
     }
     if (mode == kModeRender)
         return a.sd.samples > 1u && WCPT_MK_PRIMARY_REUSE
-                   ? launch_mega<false, false, 1, PAIRS, SINGLE, true>(a, mk, stream, tilesX, tiles)
-                   : launch_mega<false, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
-    if (mode == kModeCount) return launch_mega<true, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
-    return launch_mega<true, true, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles);
+                   ? launch_mega<false, false, 1, PAIRS, SINGLE, true>(a, mk, stream, tilesX, tiles, list, grid)
+                   : launch_mega<false, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles, list, grid);
+    if (mode == kModeCount) return launch_mega<true, false, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles, list, grid);
+    return launch_mega<true, true, 1, PAIRS, SINGLE>(a, mk, stream, tilesX, tiles, list, grid);
 }
 
-hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream)
+hipError_t mk_join(MkState& mk, hipStream_t stream)
+{
+    if (!mk.pending) return hipSuccess;
+    mk.pending = false;
+    hipError_t first = hipSuccess;
+    for (uint32_t p = 1; p < kMkPipes; p++) { /* pipe 0 is the context's stream itself */
+        hipError_t e = hipEventRecord(mk.join[p], mk.pipe[p]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, mk.join[p], 0);
+        if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    return first;
+}
+
+/* Frame overlap: a launch leaves its last round of waves with fewer and fewer tiles (the cost order puts the shortest
+ * last) and the next frame's launch on the same stream cannot start before the last one ends -- the in-order queue
+ * sets each dispatch's barrier bit, and gfx9 has no any-order launch (hip_ext.h). Two contexts rendering the Cornell
+ * box round-robin finish 5.0 % more frames than one (0.3441 against 0.3614 ms, tools/stream_overlap.py,
+ * profiles/r06_stream_overlap.log): that tail, overlapped by the other stream's work. Here one context does it with
+ * two pipes: each takes half the cost-ordered tiles (every other position of the order, so both halves cost alike),
+ * pipe 0 on the context's stream and pipe 1 on a stream of its own (one stream more per context: a one-rank group's
+ * communication stream still fits the device's four hardware queues), and a pipe's next frame queues behind its own
+ * previous frame only. A pixel belongs to the
+ * same pipe in every frame while the order stands, so its frames accumulate in order; a re-sort, a new geometry,
+ * another kernel or any other entry point first joins both pipes into the context's stream (mk_join). From 2 rounds of
+ * resident waves up (auto): a one-round launch has no last round to fill. */
+constexpr uint32_t kMkOverlapMinTilesPerCu = 32;
+
+hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream, int overlap)
 {
     const uint32_t tilesX = (a.W + dev::kTileW - 1u) / dev::kTileW;
     const uint32_t tilesY = (a.rows + dev::kTileH - 1u) / dev::kTileH;
     const uint32_t tiles = tilesX * tilesY;
-    if (tiles == 0) return hipSuccess;
     if (mk.cus == 0) { /* CU count of the context's device, cached per context */
         int dev = 0;
         hipError_t e = hipGetDevice(&dev);
@@ -554,23 +605,58 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
         if (e != hipSuccess) return e;
     }
     const bool cost_order = mode == kModeRender && a.mk_tile_order == 2;
+    const bool same_geometry = mk.geom_tiles == tiles && mk.geom_w == a.W && mk.geom_rows == a.rows &&
+                               mk.geom_y0 == a.y0 && mk.geom_shift == a.row_shift && mk.geom_gap == a.row_gap;
+    const bool pipes = overlap != 0 && cost_order && same_geometry && mk.order_valid && mk.split_valid && tiles >= 2u &&
+                       (overlap == 2 || (uint64_t)tiles >= (uint64_t)kMkOverlapMinTilesPerCu * (uint64_t)mk.cus);
+    hipError_t e = hipSuccess;
+    if (mk.pending && !(pipes && mk.pending_tiles == tiles)) {
+        e = mk_join(mk, stream);
+        if (e != hipSuccess) return e;
+    }
+    if (tiles == 0) return hipSuccess;
     if (cost_order) {
-        hipError_t e = cost_order_prepare(a, mk, tiles, stream);
+        e = cost_order_prepare(a, mk, tiles, stream);
         if (e != hipSuccess) return e;
     }
     /* one draw command (the reference's case): the single-draw instantiation, without the draw loop */
     const bool single = a.sd.drawCommandCount == 1u;
-    hipError_t e;
-    if (a.pair_records)
-        e = single ? launch_mega_sk<true, true>(a, mode, stack_kind, mk, stream, tilesX, tiles)
-                   : launch_mega_sk<true, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
-    else
-        e = single ? launch_mega_sk<false, true>(a, mode, stack_kind, mk, stream, tilesX, tiles)
-                   : launch_mega_sk<false, false>(a, mode, stack_kind, mk, stream, tilesX, tiles);
+    auto launch = [&](hipStream_t s, const uint32_t* list, uint32_t grid) {
+        if (a.pair_records)
+            return single ? launch_mega_sk<true, true>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid)
+                          : launch_mega_sk<true, false>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid);
+        return single ? launch_mega_sk<false, true>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid)
+                      : launch_mega_sk<false, false>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid);
+    };
+    if (pipes) {
+        if (!mk.pending) { /* fork: pipe 1 after everything queued on the context's stream */
+            for (uint32_t p = 1; p < kMkPipes && e == hipSuccess; p++) {
+                if (!mk.pipe[p]) e = hipStreamCreateWithFlags(&mk.pipe[p], hipStreamNonBlocking);
+                if (e == hipSuccess && !mk.join[p]) e = hipEventCreateWithFlags(&mk.join[p], hipEventDisableTiming);
+            }
+            if (e == hipSuccess && !mk.fork) e = hipEventCreateWithFlags(&mk.fork, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(mk.fork, stream);
+            for (uint32_t p = 1; p < kMkPipes && e == hipSuccess; p++) e = hipStreamWaitEvent(mk.pipe[p], mk.fork, 0);
+            if (e != hipSuccess) return e;
+        }
+        const uint32_t half = (tiles + 1u) / 2u;
+        e = launch(stream, mk.split, half);
+        /* pending from the first enqueue on: a failed second launch still leaves the first to join */
+        mk.pending = true;
+        mk.pending_tiles = tiles;
+        if (e == hipSuccess) e = launch(mk.pipe[1], mk.split + half, tiles - half);
+    } else {
+        e = launch(stream, nullptr, 0);
+    }
     if (e != hipSuccess || !cost_order) return e;
-    /* sorted after renders 1, 4 and 16 of a geometry (the running averages settle), then every kResortEvery */
+    /* sorted after renders 1, 4 and 16 of a geometry (the running averages settle), then every kResortEvery; the sort
+     * rewrites the order the pipes read, so they are joined first and the next render forks after it */
     const uint32_t r = ++mk.renders;
-    if (r == 1u || r == 4u || r == 16u || r % kResortEvery == 0u) return cost_order_sort(mk, tiles, stream);
+    if (r == 1u || r == 4u || r == 16u || r % kResortEvery == 0u) {
+        e = mk_join(mk, stream);
+        if (e != hipSuccess) return e;
+        return cost_order_sort(mk, tiles, stream);
+    }
     return hipSuccess;
 }
 

@@ -1129,8 +1129,25 @@ static hipError_t pipe_iterate(const LaunchArgs& a, int mode, WfState& s, uint32
     return hipSuccess;
 }
 
+#ifndef WCPT_WF_START_TOGETHER
+#define WCPT_WF_START_TOGETHER 0
+#endif
+
+hipError_t wf_join(WfPipes& w, hipStream_t stream)
+{
+    if (!w.pending) return hipSuccess;
+    w.pending = false;
+    hipError_t first = hipSuccess;
+    for (uint32_t j = 1; j < w.pending_pipes; j++) {
+        hipError_t e = hipEventRecord(w.join[j], w.aux[j]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, w.join[j], 0);
+        if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    return first;
+}
+
 hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes, bool sort_rays, int lds_stack,
-                            hipStream_t stream)
+                            hipStream_t stream, int overlap)
 {
     const uint32_t tilesX = (a.W + 7u) / 8u;
     const uint32_t tilesY = (a.rows + 7u) / 8u;
@@ -1195,6 +1212,18 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     if (K > 1) trace_grid = trace_grid / K > 0 ? trace_grid / K : 1u;
 #endif
     const uint32_t persist_grid = persist ? max(1u, persist_full / K) : 0u;
+    /* Frame overlap (WCPT_OPTION_FRAME_OVERLAP; the megakernel's in pt_kernels.hip launch_megakernel): pipeline j
+     * owns the tiles t % K == j, so while K and the frame's tiles stay, this render's pipelines need not wait for the
+     * previous render's other pipelines -- each continues on its own stream, and the context's stream is joined to
+     * them only when another entry point needs it (wf_join). On the per-bounce launches that recovers the frame's
+     * ragged end (c3: its three pipelines end 0.3-0.5 ms apart, profiles/r06_c3_frame_timeline.log). */
+    const bool cont = overlap != 0 && K > 1 && !WCPT_WF_START_TOGETHER && mode == kModeRender && w.pending &&
+                      w.pending_pipes == K && w.pending_W == a.W && w.pending_rows == a.rows &&
+                      w.pending_persist == (persist_grid != 0);
+    if (w.pending && !cont) {
+        e = wf_join(w, stream);
+        if (e != hipSuccess) return e;
+    }
     e = wf_reserve_result(w, (uint64_t)a.W * a.rows);
     if (e != hipSuccess) return e;
     WfBuffers bs[kWfMaxPipes];
@@ -1219,18 +1248,17 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
             if (e != hipSuccess) return e;
         }
     }
-    e = hipEventRecord(w.fork, stream);
-    if (e != hipSuccess) return e;
-    for (uint32_t j = 1; j < K; j++) {
-        e = hipStreamWaitEvent(w.aux[j], w.fork, 0);
+    if (!cont) {
+        e = hipEventRecord(w.fork, stream);
         if (e != hipSuccess) return e;
+        for (uint32_t j = 1; j < K; j++) {
+            e = hipStreamWaitEvent(w.aux[j], w.fork, 0);
+            if (e != hipSuccess) return e;
+        }
     }
     hipError_t first = hipSuccess;
     for (uint32_t j = 0; j < K && first == hipSuccess; j++)
         first = pipe_begin(a, mode, w.pipe[j], s0, w.result, w.result + w.result_capacity, j, K, cus, j == 0 ? stream : w.aux[j], bs[j]);
-#ifndef WCPT_WF_START_TOGETHER
-#define WCPT_WF_START_TOGETHER 0
-#endif
     if (WCPT_WF_START_TOGETHER && first == hipSuccess) {
         /* every pipeline's first trace waits for all the inits: the persistent trace grids then start on an idle
          * chip together instead of the first one being placed around the other pipelines' init blocks */
@@ -1245,10 +1273,15 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     for (uint32_t j = 0; j < K && first == hipSuccess; j++)
         first = pipe_iterate(a, mode, w.pipe[j], j, K, false, ldsn, cus, trace_grid, shade_grid, persist_grid,
                              j == 0 ? stream : w.aux[j], bs[j]);
-    /* join: the context's stream continues after every pipeline (also after a failed enqueue) */
-    for (uint32_t j = 1; j < K; j++) {
-        e = hipEventRecord(w.join[j], w.aux[j]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(stream, w.join[j], 0);
+    /* join: the context's stream continues after every pipeline (also after a failed enqueue) -- now, or with the
+     * frame overlap when another entry point needs the stream (wf_join) */
+    w.pending = true;
+    w.pending_pipes = K;
+    w.pending_W = a.W;
+    w.pending_rows = a.rows;
+    w.pending_persist = persist_grid != 0;
+    if (!overlap || mode != kModeRender || first != hipSuccess) {
+        e = wf_join(w, stream);
         if (e != hipSuccess && first == hipSuccess) first = e;
     }
     return first;

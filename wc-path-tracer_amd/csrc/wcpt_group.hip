@@ -1097,6 +1097,10 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
      * a simulated device): payload reuse behind the previous transfer, renders, ready events, transfers, sent events */
     g->plan_state.resize(nl);
     for (size_t i = 0; i < nl; i++) {
+        /* a sender records its ready event on the render stream after every render, and the root without overlap
+         * receives on it: those contexts' frames are joined every frame, so no frame overlap there */
+        wcpt::set_overlap_suppressed(g->local[i].ctx, exchange && g->transport != WCPT_GROUP_TRANSPORT_DIRECT &&
+                                                          (g->local[i].rank != g->root || !g->overlap));
         g->plan_state[i].rank = g->local[i].rank;
         for (int k = 0; k < kPayloadBuffers; k++) g->plan_state[i].sent_pending[k] = g->local[i].sent_pending[k];
     }

@@ -167,6 +167,9 @@ struct wcpt_context {
     int wf_pipes = WCPT_WF_PIPES_DEFAULT; /* WCPT_OPTION_WF_PIPES (0 = by queue length, pt_wavefront.hip launch_wavefront) */
     int pair_records = -1;             /* WCPT_OPTION_PAIR_RECORDS: -1 auto, 0 singles, 1 pairs (megakernel) */
     int mk_tile_order = 2;             /* WCPT_OPTION_MK_TILE_ORDER: auto */
+    int frame_overlap = 1;             /* WCPT_OPTION_FRAME_OVERLAP: auto */
+    bool overlap_suppressed = false;   /* set by a group (wcpt::set_overlap_suppressed) */
+    bool prep_missed = false;          /* the last render's preparation missed its cache (prepare_tri_records) */
     uint64_t generation = 0;           /* bumped by every buffer alloc / upload / free and every option change */
     /* Frame preparation of the last render (prepare_tri_records) and the last validation (render_validate), reused
      * while nothing they read can have changed: the same draw-command address and count, no buffer allocated,
@@ -231,11 +234,28 @@ int hip_fail(wcpt_context* ctx, hipError_t e, const char* what)
         if (_e != hipSuccess) return hip_fail((ctx), _e, (what)); \
     } while (0)
 
-int bind(wcpt_context* ctx)
+/* the context's device current, without touching its stream (render_common: a render may continue the overlap) */
+int bind_device(wcpt_context* ctx)
 {
     if (!ctx) return set_error(nullptr, WCPT_ERROR_INVALID_HANDLE, "null context");
     HIP_TRY(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     return WCPT_SUCCESS;
+}
+
+/* Frames the frame-overlap pipes hold (MkState::pending) are joined into the context's stream before anything else
+ * is queued there or waited for: every entry point but a render binds through here, and so does the group's access
+ * to the stream (context_stream), so stream order is as if each render had run on the stream itself. */
+int join_pending(wcpt_context* ctx)
+{
+    if (ctx->mk.pending) HIP_TRY(ctx, wcpt::mk_join(ctx->mk, ctx->stream), "frame overlap join");
+    if (ctx->wf.pending) HIP_TRY(ctx, wcpt::wf_join(ctx->wf, ctx->stream), "frame overlap join (wavefront)");
+    return WCPT_SUCCESS;
+}
+
+int bind(wcpt_context* ctx)
+{
+    const int rc = bind_device(ctx);
+    return rc ? rc : join_pending(ctx);
 }
 
 Buffer* find_buffer(wcpt_context* ctx, wcpt_buffer h)
@@ -325,9 +345,16 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         a.wf_fast = pc.wf_fast;
         ctx->kernel_run = pc.kernel_run;
         a.tri_records = ctx->d_tri_table;
+        ctx->prep_missed = false;
         return WCPT_SUCCESS;
     }
     pc.valid = false;
+    /* the preparation below may rebuild records that pending frames read, and queues its work on the stream; the
+     * frame that follows runs on the stream itself (render_common): a camera that moves every frame rebuilds the
+     * primary-ray records every frame, and a fork and a join per frame would cost more than the overlap returns */
+    ctx->prep_missed = true;
+    int jrc = join_pending(ctx);
+    if (jrc) return jrc;
     const uint64_t dbytes = (uint64_t)n * sizeof(wcpt_draw_command);
     uint64_t off = 0;
     Buffer* db = buffer_at(ctx, draws, off);
@@ -547,8 +574,17 @@ int check_render_args(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t 
 int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                   uint64_t draws, int mode)
 {
-    int rc = bind(ctx);
+    int rc = bind_device(ctx);
     if (rc) return rc;
+    /* frame overlap (WCPT_OPTION_FRAME_OVERLAP, pt_kernels.hip launch_megakernel): renders only, on the context's own
+     * stream (work the application queues on a stream of its own could not be ordered behind the pipes), and not
+     * under per-render timing events (they bracket each frame on the stream) */
+    int overlap = (mode == wcpt::kModeRender && ctx->stream == ctx->own_stream && !ctx->overlap_suppressed &&
+                   !(ctx->profiling && !ctx->profile_region)) ? ctx->frame_overlap : 0;
+    if (!overlap) {
+        rc = join_pending(ctx);
+        if (rc) return rc;
+    }
     rc = check_render_args(ctx, scene, materials, spheres, draws, mode);
     if (rc) return rc;
     wcpt::LaunchArgs a;
@@ -611,18 +647,29 @@ int render_common(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t mate
         ctx->events_used++;
         HIP_TRY(ctx, hipEventRecord(e0, ctx->stream), "hipEventRecord");
     }
+    ctx->prep_missed = false;
     rc = prepare_tri_records(ctx, *scene, draws, a);
     if (rc) return rc;
+    if (ctx->prep_missed) overlap = 0;
+    /* the other kernel's pending frames (the same image) first */
+    if (ctx->kernel_run != WCPT_KERNEL_MEGAKERNEL && ctx->mk.pending)
+        HIP_TRY(ctx, wcpt::mk_join(ctx->mk, ctx->stream), "frame overlap join");
+    if (ctx->kernel_run != WCPT_KERNEL_WAVEFRONT && ctx->wf.pending)
+        HIP_TRY(ctx, wcpt::wf_join(ctx->wf, ctx->stream), "frame overlap join (wavefront)");
 #if WCPT_MK_TIMERS
     /* tools-only build: the render's megakernel adds its phase timers to the counters (wcpt_read_diagnostics) */
+    rc = join_pending(ctx);
+    if (rc) return rc;
     if (mode == wcpt::kModeRender && ctx->kernel_run == WCPT_KERNEL_MEGAKERNEL)
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream),
                 "hipMemsetAsync(timers)");
 #endif
     hipError_t e = hipSuccess;
     switch (ctx->kernel_run) {
-    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->mk, ctx->stream); break;
-    case WCPT_KERNEL_WAVEFRONT: e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->wf_pipes, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream); break;
+    case WCPT_KERNEL_MEGAKERNEL: e = wcpt::launch_megakernel(a, mode, ctx->stack_kind, ctx->mk, ctx->stream, overlap); break;
+    case WCPT_KERNEL_WAVEFRONT:
+        e = wcpt::launch_wavefront(a, mode, ctx->wf, ctx->wf_pipes, ctx->sort_rays != 0, ctx->wf_stack, ctx->stream, overlap);
+        break;
     default: return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "kernel variant %d not available", ctx->kernel_run);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "kernel launch");
@@ -650,7 +697,14 @@ int read_status(wcpt_context* ctx)
 /* Internal hooks for the multi-device group (wcpt_group.hip): a context's current stream, and error reporting
  * through the same last-error strings as the C entry points. */
 namespace wcpt {
-hipStream_t context_stream(wcpt_context* ctx) { return ctx ? ctx->stream : nullptr; }
+hipStream_t context_stream(wcpt_context* ctx)
+{
+    if (!ctx) return nullptr;
+    /* the group queues waits, copies and events here: pending overlap frames first (a failed join surfaces at the
+     * group's next stream operation or sync) */
+    (void)join_pending(ctx);
+    return ctx->stream;
+}
 int context_device(wcpt_context* ctx) { return ctx ? ctx->device : -1; }
 int context_error(wcpt_context* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
 /* A validated frame that will not be rendered (another rank's validation failed): drop its hand-off. */
@@ -662,10 +716,15 @@ void render_abandon(wcpt_context* ctx)
 /* Every check wcpt_render would make before it launches anything, with no launch: the argument checks and, per draw
  * command, the index-count bound of the record build (prepare_tri_records). A group validates all its ranks first, so
  * that an argument error cannot leave some ranks a frame ahead of the others. */
+void set_overlap_suppressed(wcpt_context* ctx, bool on)
+{
+    if (ctx) ctx->overlap_suppressed = on;
+}
+
 int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                     uint64_t draws)
 {
-    int rc = bind(ctx);
+    int rc = bind_device(ctx); /* a validation that reads nothing from the device leaves pending frames running */
     if (rc) return rc;
     rc = check_render_args(ctx, scene, materials, spheres, draws, kModeRender);
     if (rc) return rc;
@@ -686,6 +745,8 @@ int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t ma
     } else {
         /* read from the device (the application may write draw commands behind the runtime); the render that follows
          * takes these (prepare_tri_records), so a frame reads them once */
+        rc = join_pending(ctx);
+        if (rc) return rc;
         HIP_TRY(ctx, hipMemcpyAsync(dc.data(), reinterpret_cast<const void*>(draws), dbytes, hipMemcpyDeviceToHost,
                                     ctx->stream), "hipMemcpyAsync(draw commands)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(draw commands)");
@@ -824,6 +885,7 @@ int wcpt_destroy(wcpt_context* ctx)
 {
     if (!ctx) return WCPT_SUCCESS;
     (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)join_pending(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->buffers)
         if (kv.second.raw) (void)hipFree(kv.second.raw);
@@ -897,6 +959,10 @@ int wcpt_set_option(wcpt_context* ctx, int option, int value)
     case WCPT_OPTION_MK_TILE_ORDER:
         if (value < 0 || value > 6) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "tile order %d", value);
         ctx->mk_tile_order = value;
+        return WCPT_SUCCESS;
+    case WCPT_OPTION_FRAME_OVERLAP:
+        if (value < 0 || value > 2) return set_error(ctx, WCPT_ERROR_INVALID_ARGUMENT, "frame overlap %d", value);
+        ctx->frame_overlap = value;
         return WCPT_SUCCESS;
     case WCPT_OPTION_PACKED_REFS:
         ctx->packed_refs = value ? 1 : 0;

@@ -56,6 +56,7 @@ OPTION_PROFILE_REGION = 11
 OPTION_WF_FETCH = 12
 OPTION_WF_PERSIST = 13
 OPTION_GATHER_FRAME_ROWS = 14
+OPTION_FRAME_OVERLAP = 15
 DEFAULT_WF_PIPES = 0  # wcpt_runtime.hip: by queue length (2 or 3)
 
 # gather payload formats (wcpt_set_gather_output, wcpt_group_set_output)
