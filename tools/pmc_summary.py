@@ -13,13 +13,17 @@ import json
 import os
 from collections import defaultdict
 
+from sq_summary import grid_size
 
-def load(d):
+
+def load(d, grids=None):
     per = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
             per[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            if grids is not None:
+                grids[name][row["Counter_Name"]] += grid_size(row)
     return per
 
 
@@ -39,8 +43,12 @@ def main():
                     help="whole-frame mode (wavefront: several kernels per frame): --kernel is a comma list of "
                          "kernel filters whose counters are SUMMED over all their dispatches and divided by the "
                          "dispatch count of this kernel (one per frame, e.g. 'wf_init<false')")
+    ap.add_argument("--frame-grid", type=int, default=0,
+                    help="work-items of --kernel per frame: per-FRAME counters, the dispatches' sums scaled by frame "
+                         "grid / dispatched grid (a megakernel frame under the frame overlap is two launches)")
     a = ap.parse_args()
-    per = load(a.dir)
+    grids = defaultdict(lambda: defaultdict(float)) if a.frame_grid else None
+    per = load(a.dir, grids)
     out = {}
     if a.frame_kernel:
         # frames per counter: each counter comes from its own --pmc pass (a separate run, whose untimed settle phase
@@ -60,6 +68,15 @@ def main():
                 out[c] = out.get(c, 0.0) + sum(vals) / (frames[c] / a.per_frame)
         if not out:
             raise SystemExit(f"no dispatches of {a.kernel} in {a.dir}")
+    elif a.frame_grid:
+        tot, gr = defaultdict(float), defaultdict(float)
+        for name, ctrs in per.items():
+            if a.kernel not in name:
+                continue
+            for c, vals in ctrs.items():
+                tot[c] += sum(vals)
+                gr[c] += grids[name][c]
+        out = {c: tot[c] * a.frame_grid / gr[c] for c in tot}
     else:
         for name, ctrs in per.items():
             if a.kernel not in name:
@@ -70,7 +87,7 @@ def main():
         raise SystemExit(f"no dispatches of {a.kernel} in {a.dir}")
     d = dict(out)
     if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
-        key = "hbm_bytes_per_frame" if a.frame_kernel else "hbm_bytes_per_launch"
+        key = "hbm_bytes_per_frame" if (a.frame_kernel or a.frame_grid) else "hbm_bytes_per_launch"
         d[key] = int((2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024)
     if "SQ_ACTIVE_INST_VALU" in out and "SQ_THREAD_CYCLES_VALU" in out and out["SQ_ACTIVE_INST_VALU"]:
         d["valu_lane_utilization"] = out["SQ_THREAD_CYCLES_VALU"] / (64.0 * out["SQ_ACTIVE_INST_VALU"])

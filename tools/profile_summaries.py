@@ -32,6 +32,10 @@ SPEC = {
            "control between them", "wf_trace<false,wf_shade<false,wf_init<false"),
 }
 MIX = ("ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "INT32", "INT64", "CVT")
+# megakernel work-items per frame (8x8 tiles x 64 lanes of the 1920x1080 frame): under the frame overlap
+# (WCPT_OPTION_FRAME_OVERLAP) a frame is two launches of half the tiles (and one around each re-sort), so the megakernel
+# summaries count per frame by grid and time the frame as the union of its launches' intervals (frame_ms)
+FRAME_GRID = {"c2": 240 * 135 * 64, "ref": 240 * 135 * 64}
 # wavefront pipelines per frame (one wf_init each: the per-frame divisor of the PMC passes). The library picks them by
 # queue length (WCPT_OPTION_WF_PIPES 0): 3 for the 1080p atrium (2.1 M paths, 4 per resident trace lane), 2 at 4K
 PIPES = {"c3": 3, "c4": 2}
@@ -43,6 +47,30 @@ def kernel_ms(d, cfg, filt):
             if filt in row["Name"]:
                 return float(row["AverageNs"]) / 1e6
     raise SystemExit(f"{cfg}: no {filt} in the kernel stats")
+
+
+def frame_ms(d, cfg, filt, frame_grid):
+    """A frame's time from the session's kernel trace: the union of the kernel's launch intervals over the frames
+    they hold (work-items dispatched / work-items per frame). Launches of consecutive frames overlap under the frame
+    overlap, so neither a launch's duration nor their sum is a frame's time."""
+    iv, work = [], 0.0
+    for f in glob.glob(os.path.join(d, f"prof_{cfg}", "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if filt in row["Kernel_Name"]:
+                iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+                work += float(row["Grid_Size_X"]) * float(row.get("Grid_Size_Y") or 1) * float(row.get("Grid_Size_Z") or 1)
+    if not iv:
+        raise SystemExit(f"{cfg}: no {filt} in the kernel trace")
+    iv.sort()
+    busy, s0, e0 = 0, iv[0][0], iv[0][1]
+    for s, e in iv[1:]:
+        if s > e0:
+            busy += e0 - s0
+            s0, e0 = s, e
+        else:
+            e0 = max(e0, e)
+    busy += e0 - s0
+    return busy / 1e6 / (work / frame_grid)
 
 
 def counters(d, cfg, filt):
@@ -67,19 +95,27 @@ def main():
         base = cfg[:-len("_orbit")] if cfg.endswith("_orbit") else cfg
         camera = "orbit" if base != cfg else "still"
         kid, filt, lpf, bound, resource, frame_filters = SPEC[base]
-        ms = kernel_ms(a.dir, cfg, filt)
-        src = (a.source or tag) + f" (tools/gpu_sq.sh; {filt.split('<')[0]} {ms:.4f} ms avg from " \
-                                  f"the session's kernel stats; camera {camera})"
+        fg = FRAME_GRID.get(base, 0)
+        if fg:
+            ms = frame_ms(a.dir, cfg, filt, fg)
+            src = (a.source or tag) + f" (tools/gpu_sq.sh; {filt.split('<')[0]} {ms:.4f} ms per frame: the union of " \
+                                      f"its launch intervals in the session's kernel trace over the frames they hold; " \
+                                      f"camera {camera})"
+        else:
+            ms = kernel_ms(a.dir, cfg, filt)
+            src = (a.source or tag) + f" (tools/gpu_sq.sh; {filt.split('<')[0]} {ms:.4f} ms avg from " \
+                                      f"the session's kernel stats; camera {camera})"
         py = sys.executable
         subprocess.run([py, os.path.join(ROOT, "tools", "sq_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--kernel",
                         filt, "--ms", str(ms), "--launches-per-frame", str(lpf), "--config", base, "--camera", camera, "--kernel-id",
                         str(kid), "--bound", bound, "--resource", resource, "--source", src, "--build-id", build,
-                        "--json", os.path.join(a.out, f"sq_{cfg}.json")], check=True, stdout=subprocess.DEVNULL)
+                        "--json", os.path.join(a.out, f"sq_{cfg}.json")] + (["--frame-grid", str(fg)] if fg else []),
+                       check=True, stdout=subprocess.DEVNULL)
         pm = [py, os.path.join(ROOT, "tools", "pmc_summary.py"), os.path.join(a.dir, f"sq_{cfg}"), "--config", base,
               "--camera", camera,
               "--kernel-id", str(kid), "--build-id", build, "--json", os.path.join(a.out, f"pmc_traffic_{cfg}.json")]
         pm += (["--kernel", frame_filters, "--frame-kernel", "wf_init<false", "--per-frame", str(PIPES[base])]
-               if frame_filters else ["--kernel", filt])
+               if frame_filters else ["--kernel", filt] + (["--frame-grid", str(fg)] if fg else []))
         subprocess.run(pm, check=True, stdout=subprocess.DEVNULL)
         m, n = counters(a.dir, cfg, filt)
         tot = m.get("SQ_INSTS_VALU")

@@ -15,6 +15,15 @@ import os
 from collections import defaultdict
 
 
+def grid_size(row) -> float:
+    """Work-items of a dispatch row of a rocprofv3 counter_collection.csv."""
+    for k in ("Grid_Size", "Grid_Size_X"):
+        if row.get(k):
+            return float(row[k]) * float(row.get("Grid_Size_Y") or 1) * float(row.get("Grid_Size_Z") or 1) \
+                if k == "Grid_Size_X" else float(row[k])
+    raise SystemExit("counter CSV without a grid-size column (needed for --frame-grid)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -32,13 +41,22 @@ def main():
                     help="the binding resource bench.py's roofline prices against")
     ap.add_argument("--resource", default=None, help="one-line description of the binding resource")
     ap.add_argument("--source", default=None, help="where the passes came from (round, script, kernel time)")
+    ap.add_argument("--frame-grid", type=int, default=0,
+                    help="work-items of the kernel per frame: counters are then per FRAME, summed over the dispatches "
+                         "and scaled by frame grid / dispatched grid (the frame overlap splits a megakernel frame into "
+                         "two launches of half the tiles), and --ms is the frame's time")
     a = ap.parse_args()
     per = defaultdict(list)
+    grid = defaultdict(float)
     for f in glob.glob(os.path.join(a.dir, "p*", "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if a.kernel in row.get("Kernel_Name", ""):
                 per[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    m = {k: sum(v) / len(v) for k, v in per.items()}
+                grid[row["Counter_Name"]] += grid_size(row) if a.frame_grid else 0.0
+    if a.frame_grid:
+        m = {k: sum(v) * a.frame_grid / grid[k] for k, v in per.items()}
+    else:
+        m = {k: sum(v) / len(v) for k, v in per.items()}
     out = {"kernel": a.kernel, "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())}}
     cycles = a.ms * 1e-3 * a.cycles_per_sec
     if "SQ_INSTS_VALU" in m:
@@ -52,7 +70,10 @@ def main():
         out["l2_hit_rate"] = round(m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 3)
     if "SQ_THREAD_CYCLES_VALU" in m and "SQ_ACTIVE_INST_VALU" in m:
         out["lane_utilisation_valu"] = round(m["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * m["SQ_ACTIVE_INST_VALU"]), 3)
-    out["launches_per_frame"] = a.launches_per_frame
+    out["launches_per_frame"] = 1.0 if a.frame_grid else a.launches_per_frame
+    if a.frame_grid:
+        out["per_frame"] = (f"counters_per_launch hold one frame's counts: the dispatches' sums x {a.frame_grid} "
+                            f"work-items per frame / the work-items dispatched")
     for k in ("config", "camera", "bound", "resource", "source"):
         if getattr(a, k) is not None:
             out[k] = getattr(a, k)
