@@ -138,8 +138,9 @@ extern "C" {
  * pipe's next frame starts in the other's last round of waves instead of behind the whole frame. Every other entry
  * point (wcpt_sync, readback, composite, profile end, buffer calls, a group's exchange ...) first orders the context's
  * stream after both pipes, so what it sees or queues is as if each render had run on the stream; hence only on the
- * context's own stream (not after wcpt_set_stream) and not under per-render timing events. 1 (default): from two rounds
- * of resident waves up (a 1920x1080 frame, not an 8-way row block); 0 off; 2 whenever the tiles are cost-ordered.
+ * context's own stream (not after wcpt_set_stream) and not under per-render timing events. 1 (default): megakernel
+ * launches from 1.5 rounds of resident waves up (a 1920x1080 frame or its 2- and 4-way row blocks, not an 8-way block),
+ * wavefront frames of several pipelines; 0 off; 2 whenever the tiles are cost-ordered.
  * Same results. Added under ABI 4. */
 #define WCPT_OPTION_FRAME_OVERLAP 15
 

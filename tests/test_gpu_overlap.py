@@ -144,17 +144,24 @@ def test_overlap_interleaved_calls_equal_plain_stream(kernel):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("n", [1, 2])
-def test_overlap_in_a_group_equals_plain(n, kernel):
-    """A one-process COPY group on the one GPU whose contexts overlap their renders: the root's presented frames and
-    every rank's block equal the group without overlap (the senders' per-frame ready events join their pipes; the
-    root's pipes run on between the exchanges)."""
+@pytest.mark.parametrize("n,transport,gov,stripe", [(1, "copy", 1, 0), (2, "copy", 1, 0), (3, "copy", 1, 0),
+                                                    (3, "copy", 0, 0), (2, "direct", 1, 0), (3, "copy", 1, 8)])
+def test_overlap_in_a_group_equals_plain(n, transport, gov, stripe, kernel):
+    """A one-process group on the one GPU whose contexts overlap their renders: the root's presented frames and every
+    rank's block equal the group without overlap. With communication streams (GROUP_OPTION_OVERLAP 1) a sender's pipes
+    run on: each frame is fenced by an event on every stream holding part of it, and the next frame's streams wait for
+    the payload's previous transfer; with transfers in line (0) the group keeps the overlap off; DIRECT renders write
+    the root's frame themselves; stripes interleave the ranks' rows."""
     s = get_scene("cornell")
     W, H, frames = 72, 45, range(10)
     fmt = T.PAYLOAD_RGBA32F
+    tr = {"copy": T.GROUP_TRANSPORT_COPY, "direct": T.GROUP_TRANSPORT_DIRECT}[transport]
     res = {}
     for ov in (2, 0):
-        with wcpt.Group([0] * n, root=0, transport=T.GROUP_TRANSPORT_COPY) as g:
+        with wcpt.Group([0] * n, root=0, transport=tr) as g:
+            g.set_option(T.GROUP_OPTION_OVERLAP, gov)
+            if stripe:
+                g.set_option(T.GROUP_OPTION_ROW_STRIPE, stripe)
             devs = []
             for r in range(n):
                 c = g.context(r)

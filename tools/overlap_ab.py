@@ -3,6 +3,7 @@ through a one-rank group (its communication stream on or off: GROUP_OPTION_OVERL
 on, interleaved rounds; ms/frame from the host clock between two synchronisations.
 
     python tools/overlap_ab.py [--config c2] [--frames 200] [--rounds 3] [--modes ctx,group,group-inline]
+        [--values 0,1] [--block N,r]    (--block: one rank's row block of an N-way split, ctx mode)
 """
 import argparse
 import os
@@ -27,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--modes", default="ctx,group,group-inline")
     ap.add_argument("--values", default="0,1")
+    ap.add_argument("--block", default=None, help="N,r: render only rank r's row block of an N-way split (ctx mode)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
@@ -52,6 +54,10 @@ def main():
                     render, sync = (lambda sd: g.render(sd, *addr)), g.sync
                 else:
                     ctx.create_screen(W, H)
+                    if a.block:
+                        from wcpt.dist import row_block
+                        n, rk = (int(x) for x in a.block.split(","))
+                        ctx.set_row_range(*row_block(H, n, rk))
                     render, sync = (lambda sd: ctx.render(sd, *dev.addresses())), ctx.sync
                 for sd in sds[:20]:
                     render(sd)

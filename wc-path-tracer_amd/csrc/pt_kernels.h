@@ -156,6 +156,11 @@ void mk_release(MkState& mk);
 /* A group suppresses the overlap on a context whose frames it joins every frame anyway (a sender's ready event, the
  * root's in-line receives): there a fork and a join per frame would cost more than the tail they hide. */
 void set_overlap_suppressed(wcpt_context* ctx, bool on);
+/* The streams that hold the context's last frame and will run its next one: the context's stream, then the overlap
+ * pipes' streams while frames are pending on them (at most kMaxFrameStreams). A group fences a frame's payload with an
+ * event on each (and makes each wait for the payload's previous transfer) instead of joining the pipes every frame. */
+constexpr int kMaxFrameStreams = 4;
+int context_frame_streams(wcpt_context* ctx, hipStream_t* out, int cap);
 hipError_t mk_join(MkState& mk, hipStream_t stream);
 
 /* Launch modes: render the frame; count the reference algorithm's work (no image write); count + SIMD

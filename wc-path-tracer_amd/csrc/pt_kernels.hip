@@ -589,9 +589,10 @@ hipError_t mk_join(MkState& mk, hipStream_t stream)
  * communication stream still fits the device's four hardware queues), and a pipe's next frame queues behind its own
  * previous frame only. A pixel belongs to the
  * same pipe in every frame while the order stands, so its frames accumulate in order; a re-sort, a new geometry,
- * another kernel or any other entry point first joins both pipes into the context's stream (mk_join). From 2 rounds of
- * resident waves up (auto): a one-round launch has no last round to fill. */
-constexpr uint32_t kMkOverlapMinTilesPerCu = 32;
+ * another kernel or any other entry point first joins both pipes into the context's stream (mk_join). Auto: from 1.5
+ * rounds of resident waves up (c2 4-way blocks, 2 rounds: 0.1168 -> 0.0916 ms, 2-way 0.1976 -> 0.1759 ms; an 8-way block
+ * is one round, and there the overlap measured +0.9 %; profiles/r06_block_overlap.log). */
+constexpr uint32_t kMkOverlapMinTilesPerCu = 24;
 
 hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkState& mk, hipStream_t stream, int overlap)
 {

@@ -71,6 +71,9 @@ struct LocalRank {
     uint64_t payload_cap[kPayloadBuffers] = {};
     hipEvent_t ready[kPayloadBuffers] = {};  /* the render that wrote payload[b] has finished */
     hipEvent_t sent[kPayloadBuffers] = {};   /* the transfer that read payload[b] has finished */
+    /* with the frame overlap, `ready` covers the context's stream and these its pipe streams (created on first use) */
+    hipEvent_t ready_pipe[kPayloadBuffers][wcpt::kMaxFrameStreams - 1] = {};
+    int ready_n[kPayloadBuffers] = {};
     bool sent_pending[kPayloadBuffers] = {};
     std::vector<void*> retired;              /* replaced payload buffers, freed at the next group-wide wait */
     void* stage = nullptr;                   /* root, RCCL with row stripes: every sender's block back to back */
@@ -420,10 +423,16 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
             if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
         }
         switch (st.op) {
-        case plan::kWaitSent:
+        case plan::kWaitSent: {
+            /* every stream the next frame may render on waits for the payload's previous transfer: the context's
+             * stream and, while the frame overlap holds frames on them, its pipe streams (no join) */
             PHIP(hipSetDevice(lr.device), "hipSetDevice");
-            PHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.sent[st.buffer], 0), "hipStreamWaitEvent(sent)");
+            hipStream_t fs[wcpt::kMaxFrameStreams];
+            const int n = wcpt::context_frame_streams(lr.ctx, fs, wcpt::kMaxFrameStreams);
+            for (int k = 0; k < n; k++)
+                PHIP(hipStreamWaitEvent(fs[k], lr.sent[st.buffer], 0), "hipStreamWaitEvent(sent)");
             break;
+        }
         case plan::kSetOutput: {
             const uint64_t bytes = block_bytes(lr.rank);
             if (!lr.payload[st.buffer] || lr.payload_cap[st.buffer] < bytes)
@@ -440,13 +449,27 @@ int run_steps(wcpt_group* g, int only, const wcpt_scene_data* scene, const uint6
             if (rc) return rc;
             break;
         }
-        case plan::kRecordReady:
+        case plan::kRecordReady: {
+            /* the frame is complete when the context's stream and every pipe stream holding part of it are: one event
+             * on each (in line transfers run on the render stream, whose frames are joined: one stream) */
             PHIP(hipSetDevice(lr.device), "hipSetDevice");
-            PHIP(hipEventRecord(lr.ready[st.buffer], stream_of(lr, st.stream)), "hipEventRecord(ready)");
+            hipStream_t fs[wcpt::kMaxFrameStreams];
+            const int n = g->overlap ? wcpt::context_frame_streams(lr.ctx, fs, wcpt::kMaxFrameStreams) : 0;
+            PHIP(hipEventRecord(lr.ready[st.buffer], n ? fs[0] : stream_of(lr, st.stream)), "hipEventRecord(ready)");
+            for (int k = 1; k < n; k++) {
+                hipEvent_t& ev = lr.ready_pipe[st.buffer][k - 1];
+                if (!ev) PHIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(ready)");
+                PHIP(hipEventRecord(ev, fs[k]), "hipEventRecord(ready)");
+            }
+            lr.ready_n[st.buffer] = n > 1 ? n : 1;
             break;
+        }
         case plan::kCommWaitReady:
             PHIP(hipSetDevice(lr.device), "hipSetDevice");
             PHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.ready[st.buffer], 0), "hipStreamWaitEvent(ready)");
+            for (int k = 1; k < lr.ready_n[st.buffer]; k++)
+                PHIP(hipStreamWaitEvent(stream_of(lr, st.stream), lr.ready_pipe[st.buffer][k - 1], 0),
+                     "hipStreamWaitEvent(ready)");
             break;
         case plan::kSend:
             if (g->transport == WCPT_GROUP_TRANSPORT_COPY) {
@@ -865,6 +888,8 @@ int wcpt_group_destroy(wcpt_group* g)
             if (lr.payload[b]) (void)hipFree(lr.payload[b]);
             if (lr.ready[b]) (void)hipEventDestroy(lr.ready[b]);
             if (lr.sent[b]) (void)hipEventDestroy(lr.sent[b]);
+            for (hipEvent_t ev : lr.ready_pipe[b])
+                if (ev) (void)hipEventDestroy(ev);
         }
         if (lr.stage) (void)hipFree(lr.stage);
         free_retired(lr);
@@ -1097,10 +1122,11 @@ int wcpt_group_render(wcpt_group* g, const wcpt_scene_data* scene, const uint64_
      * a simulated device): payload reuse behind the previous transfer, renders, ready events, transfers, sent events */
     g->plan_state.resize(nl);
     for (size_t i = 0; i < nl; i++) {
-        /* a sender records its ready event on the render stream after every render, and the root without overlap
-         * receives on it: those contexts' frames are joined every frame, so no frame overlap there */
+        /* transfers in line with the renders (GROUP_OPTION_OVERLAP 0) run on the render stream, which joins the
+         * context's frames every frame: no frame overlap there. With the communication streams a sender fences each
+         * frame on every stream that holds part of it (kRecordReady) and its pipes run on */
         wcpt::set_overlap_suppressed(g->local[i].ctx, exchange && g->transport != WCPT_GROUP_TRANSPORT_DIRECT &&
-                                                          (g->local[i].rank != g->root || !g->overlap));
+                                                          !g->overlap);
         g->plan_state[i].rank = g->local[i].rank;
         for (int k = 0; k < kPayloadBuffers; k++) g->plan_state[i].sent_pending[k] = g->local[i].sent_pending[k];
     }

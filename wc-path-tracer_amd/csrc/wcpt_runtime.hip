@@ -721,6 +721,18 @@ void set_overlap_suppressed(wcpt_context* ctx, bool on)
     if (ctx) ctx->overlap_suppressed = on;
 }
 
+int context_frame_streams(wcpt_context* ctx, hipStream_t* out, int cap)
+{
+    if (!ctx || cap < 1) return 0;
+    int n = 0;
+    out[n++] = ctx->stream;
+    if (ctx->mk.pending)
+        for (uint32_t p = 1; p < wcpt::kMkPipes && n < cap; p++) out[n++] = ctx->mk.pipe[p];
+    if (ctx->wf.pending)
+        for (uint32_t j = 1; j < ctx->wf.pending_pipes && n < cap; j++) out[n++] = ctx->wf.aux[j];
+    return n;
+}
+
 int render_validate(wcpt_context* ctx, const wcpt_scene_data* scene, uint64_t materials, uint64_t spheres,
                     uint64_t draws)
 {
