@@ -190,6 +190,56 @@ def test_overlap_in_a_group_equals_plain(n, transport, gov, stripe, kernel):
         assert np.array_equal(_bits(x), _bits(y))
 
 
+def _moving_camera_frames(ov, s, W, H, n_frames, upload_at=None):
+    """Progressive frames while the camera moves every frame, then stays, then moves again (the editor's drag); the
+    megakernel with pair records, so every frame's first segments use the primary-ray records of its position."""
+    import ctypes
+    cams = []
+    for f in range(n_frames):
+        cam = wcpt.Camera()
+        ctypes.pointer(cam)[0] = s.camera
+        k = f if f < 8 else (8 if f < 14 else f - 6)      # moving, still for 6 frames, moving again
+        cam.position[0] += 0.03 * k
+        cam.position[1] += 0.015 * k
+        cams.append(cam)
+    sds = [s.scene_data(W, H, max_bounce=3, samples=2, frame=f, camera=c) for f, c in enumerate(cams)]
+    with wcpt.Context(0) as ctx:
+        ctx.set_kernel(wcpt.KERNEL_MEGAKERNEL)
+        ctx.set_option(T.OPTION_PAIR_RECORDS, 1)
+        ctx.set_option(T.OPTION_FRAME_OVERLAP, ov)
+        dev = wcpt.DeviceScene(ctx, s)
+        try:
+            ctx.create_screen(W, H)
+            for f, sd in enumerate(sds):
+                if f == upload_at:   # the mesh re-uploaded: records rebuilt, both copies of the primary records follow
+                    m = s.meshes[0]
+                    ctx.buffer_upload(dev.buffers[2], np.ascontiguousarray(m.positions, dtype=np.float32))
+                ctx.render(sd, *dev.addresses())
+            ctx.sync()
+            img = ctx.readback(H)
+        finally:
+            dev.free()
+    return img, sds
+
+
+@pytest.mark.parametrize("name,W,H", [("cornell", 67, 45), ("reference_init", 96, 64)])
+def test_overlap_moving_camera(name, W, H):
+    """A camera that moves between frames: only the primary-ray records are derived again, pipe 0's copy on the
+    context's stream and pipe 1's on its own, so the overlap goes on without a join. Bit-exact against the same frames
+    without the overlap and against the oracle's accumulation; again with a mesh re-upload in the middle."""
+    import copy
+    s = get_scene(name)
+    a, sds = _moving_camera_frames(2, s, W, H, 22)
+    b, _ = _moving_camera_frames(0, s, W, H, 22)
+    assert np.array_equal(_bits(a), _bits(b))
+    acc = None
+    for sd in sds:
+        acc, _ = oracle.render_scene(copy.copy(s), W, H, sd=sd, image=acc, threads=8)
+    assert_close(a, acc)
+    c, _ = _moving_camera_frames(2, s, W, H, 22, upload_at=11)
+    assert np.array_equal(_bits(c), _bits(a))
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_overlap_auto_on_full_frame(kernel):
     """The bench's frame (Cornell, 1920x1080, 4 bounces) with the default option, where the auto rule overlaps, equals

@@ -45,6 +45,11 @@ struct LaunchArgs {
     RowMap wire_rows = {0, kContiguousShift, 0}; /* the gather output's row of local row ly (row_map.h) */
     uint32_t* status;
     unsigned long long* counters;
+    /* frame overlap (launch_megakernel): pipe 1's record table (its own copy of the primary-ray records) or null for
+     * tri_records, and the hook that brings that copy to the frame's camera on pipe 1's stream before its launch */
+    const uint64_t* tri_records_pipe1 = nullptr;
+    hipError_t (*pipe1_prepare)(void* user, hipStream_t stream) = nullptr;
+    void* pipe1_user = nullptr;
 };
 
 /* Wavefront path state (pt_wavefront.hip): structure-of-arrays in one device allocation. */

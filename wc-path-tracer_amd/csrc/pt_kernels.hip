@@ -622,12 +622,12 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
     }
     /* one draw command (the reference's case): the single-draw instantiation, without the draw loop */
     const bool single = a.sd.drawCommandCount == 1u;
-    auto launch = [&](hipStream_t s, const uint32_t* list, uint32_t grid) {
-        if (a.pair_records)
-            return single ? launch_mega_sk<true, true>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid)
-                          : launch_mega_sk<true, false>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid);
-        return single ? launch_mega_sk<false, true>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid)
-                      : launch_mega_sk<false, false>(a, mode, stack_kind, mk, s, tilesX, tiles, list, grid);
+    auto launch = [&](const LaunchArgs& la, hipStream_t s, const uint32_t* list, uint32_t grid) {
+        if (la.pair_records)
+            return single ? launch_mega_sk<true, true>(la, mode, stack_kind, mk, s, tilesX, tiles, list, grid)
+                          : launch_mega_sk<true, false>(la, mode, stack_kind, mk, s, tilesX, tiles, list, grid);
+        return single ? launch_mega_sk<false, true>(la, mode, stack_kind, mk, s, tilesX, tiles, list, grid)
+                      : launch_mega_sk<false, false>(la, mode, stack_kind, mk, s, tilesX, tiles, list, grid);
     };
     if (pipes) {
         if (!mk.pending) { /* fork: pipe 1 after everything queued on the context's stream */
@@ -641,13 +641,18 @@ hipError_t launch_megakernel(const LaunchArgs& a, int mode, int stack_kind, MkSt
             if (e != hipSuccess) return e;
         }
         const uint32_t half = (tiles + 1u) / 2u;
-        e = launch(stream, mk.split, half);
+        e = launch(a, stream, mk.split, half);
         /* pending from the first enqueue on: a failed second launch still leaves the first to join */
         mk.pending = true;
         mk.pending_tiles = tiles;
-        if (e == hipSuccess) e = launch(mk.pipe[1], mk.split + half, tiles - half);
+        if (e == hipSuccess && a.pipe1_prepare) e = a.pipe1_prepare(a.pipe1_user, mk.pipe[1]);
+        if (e == hipSuccess) {
+            LaunchArgs a1 = a;
+            if (a.tri_records_pipe1) a1.tri_records = a.tri_records_pipe1;
+            e = launch(a1, mk.pipe[1], mk.split + half, tiles - half);
+        }
     } else {
-        e = launch(stream, nullptr, 0);
+        e = launch(a, stream, nullptr, 0);
     }
     if (e != hipSuccess || !cost_order) return e;
     /* sorted after renders 1, 4 and 16 of a geometry (the running averages settle), then every kResortEvery; the sort

@@ -88,11 +88,17 @@ struct TriRecords {
     bool leaves_valid = false;
     /* primary-ray pair records (pt_device.h TriPairP) for the camera position `porigin` (bit patterns), derived from
      * the pair records of build `pbuild` */
-    void* pmem = nullptr;
+    void* pmem = nullptr;   /* two copies of pcap bytes: the context stream's, then the overlap's pipe 1's (pmem1) */
     uint64_t pcap = 0;
     bool pvalid = false;
     uint32_t porigin[3] = {0, 0, 0};
     uint64_t pbuild = 0;
+    /* pipe 1's copy (frame overlap): rebuilt on pipe 1's stream only, so neither copy is ever written while the other
+     * stream's frames read it (prep_pipe1) */
+    bool pvalid1 = false;
+    uint32_t porigin1[3] = {0, 0, 0};
+    uint64_t pbuild1 = 0;
+    void* pmem1() const { return pmem ? static_cast<char*>(pmem) + pcap : nullptr; }
 };
 
 /* Pair records (packed two-triangle tests) pay off when leaves are fat: mean triangles per leaf >= this,
@@ -197,8 +203,10 @@ struct wcpt_context {
     bool handoff_valid = false;
     std::vector<TriRecords> tri;       /* per draw command index */
     std::vector<uint64_t> tri_table;   /* host image of d_tri_table: {address, ntri} per draw */
-    uint64_t* d_tri_table = nullptr;
+    uint64_t* d_tri_table = nullptr;   /* two tables of tri_table_cap draws: the context stream's, then pipe 1's, whose
+                                        * word 4 points at the pipe-1 copy of the primary-ray records */
     uint32_t tri_table_cap = 0;        /* draws d_tri_table can hold */
+    bool prim_records = false;         /* the last preparation derived primary-ray records (table word 4) */
     std::string last_error;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -321,6 +329,39 @@ Buffer* buffer_at(wcpt_context* ctx, uint64_t addr, uint64_t& offset)
     return nullptr;
 }
 
+/* Frame overlap, pipe 1 (pt_kernels.hip launch_megakernel): before its launch, on its own stream, the pipe-1 copy of
+ * each draw's primary-ray records is derived again when it is not of the frame's camera position and records build.
+ * Only pipe 1's stream ever writes that copy and the context's stream the other, so a moving camera needs no join. */
+hipError_t prep_pipe1(void* user, hipStream_t stream)
+{
+    wcpt_context* ctx = static_cast<wcpt_context*>(user);
+    for (TriRecords& t : ctx->tri) {
+        if (!t.pvalid || t.ntri == 0) continue;
+        if (t.pvalid1 && t.pbuild1 == t.pbuild && std::memcmp(t.porigin1, t.porigin, sizeof(t.porigin)) == 0) continue;
+        float o[3];
+        std::memcpy(o, t.porigin, sizeof(o));
+        const uint64_t npairs = ((uint64_t)t.ntri + 1u) / 2u;
+        const hipError_t e = wcpt::launch_build_primary_pairs(static_cast<const char*>(t.mem) + t.pair_offset,
+                                                              (uint32_t)npairs, o[0], o[1], o[2], t.pmem1(), stream);
+        if (e != hipSuccess) return e;
+        t.pvalid1 = true;
+        t.pbuild1 = t.pbuild;
+        std::memcpy(t.porigin1, t.porigin, sizeof(t.porigin));
+    }
+    return hipSuccess;
+}
+
+void set_pipe1_records(wcpt_context* ctx, uint32_t n, wcpt::LaunchArgs& a)
+{
+    a.tri_records_pipe1 = nullptr;
+    a.pipe1_prepare = nullptr;
+    a.pipe1_user = nullptr;
+    if (!ctx->prim_records || n == 0) return; /* no primary-ray records: both pipes read the one table */
+    a.tri_records_pipe1 = ctx->d_tri_table + 5ull * ctx->tri_table_cap;
+    a.pipe1_prepare = prep_pipe1;
+    a.pipe1_user = ctx;
+}
+
 /* Derive (or reuse) the triangle records of every draw command and point a.tri_records at the table. The draw
  * commands are read from the host copy of their buffer when every byte of them was written through
  * wcpt_buffer_upload and the triangle cache is on; otherwise from the device (a synchronous copy of 32 B per draw),
@@ -345,6 +386,34 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         a.wf_fast = pc.wf_fast;
         ctx->kernel_run = pc.kernel_run;
         a.tri_records = ctx->d_tri_table;
+        set_pipe1_records(ctx, n, a);
+        ctx->prep_missed = false;
+        return WCPT_SUCCESS;
+    }
+    /* Only the camera moved (an editor drag, bench.py --camera orbit): the primary-ray records are derived again for
+     * the new position -- the context stream's copy here, behind that stream's frames; pipe 1's copy on its own stream
+     * before its launch (prep_pipe1) -- and nothing else changes, so the frame overlap goes on. */
+    if (!handoff && pc.valid && pc.gen == ctx->generation && pc.draws == draws && pc.n == n) {
+        uint32_t origin[3];
+        std::memcpy(origin, sd.position, sizeof(origin));
+        if (ctx->prim_records) {
+            for (uint32_t d = 0; d < n; d++) {
+                TriRecords& t = ctx->tri[d];
+                if (!t.pvalid || t.ntri == 0) continue;
+                const uint64_t npairs = ((uint64_t)t.ntri + 1u) / 2u;
+                HIP_TRY(ctx, wcpt::launch_build_primary_pairs(static_cast<const char*>(t.mem) + t.pair_offset,
+                                                              (uint32_t)npairs, sd.position[0], sd.position[1],
+                                                              sd.position[2], t.pmem, ctx->stream),
+                        "build_primary_pairs");
+                std::memcpy(t.porigin, origin, sizeof(origin));
+            }
+        }
+        std::memcpy(pc.origin, origin, sizeof(pc.origin));
+        a.pair_records = pc.pair_records;
+        a.wf_fast = pc.wf_fast;
+        ctx->kernel_run = pc.kernel_run;
+        a.tri_records = ctx->d_tri_table;
+        set_pipe1_records(ctx, n, a);
         ctx->prep_missed = false;
         return WCPT_SUCCESS;
     }
@@ -500,7 +569,8 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
                     t.pmem = nullptr;
                     t.pcap = 0;
                     t.pvalid = false;
-                    HIP_TRY(ctx, hipMalloc(&t.pmem, bytes), "hipMalloc(primary-ray pair records)");
+                    t.pvalid1 = false;
+                    HIP_TRY(ctx, hipMalloc(&t.pmem, 2 * bytes), "hipMalloc(primary-ray pair records)");
                     t.pcap = bytes;
                 }
                 HIP_TRY(ctx, wcpt::launch_build_primary_pairs(static_cast<const char*>(t.mem) + t.pair_offset,
@@ -525,16 +595,25 @@ int prepare_tri_records(wcpt_context* ctx, const wcpt_scene_data& sd, uint64_t d
         }
         ctx->d_tri_table = nullptr;
         ctx->tri_table_cap = 0;
-        HIP_TRY(ctx, hipMalloc(&ctx->d_tri_table, W * n * sizeof(uint64_t)), "hipMalloc(triangle record table)");
+        HIP_TRY(ctx, hipMalloc(&ctx->d_tri_table, 2 * W * n * sizeof(uint64_t)), "hipMalloc(triangle record table)");
         ctx->tri_table_cap = n;
         table_dirty = true;
     }
     if (table_dirty) {
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_tri_table, ctx->tri_table.data(), W * n * sizeof(uint64_t),
+        /* both tables: the second differs only in word 4, pipe 1's copy of the primary-ray records */
+        std::vector<uint64_t> both(2 * W * ctx->tri_table_cap, 0);
+        std::copy(ctx->tri_table.begin(), ctx->tri_table.begin() + W * n, both.begin());
+        std::copy(ctx->tri_table.begin(), ctx->tri_table.begin() + W * n, both.begin() + W * ctx->tri_table_cap);
+        for (uint32_t d = 0; d < n; d++)
+            if (ctx->tri_table[W * d + 4])
+                both[W * ctx->tri_table_cap + W * d + 4] = reinterpret_cast<uint64_t>(ctx->tri[d].pmem1());
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_tri_table, both.data(), both.size() * sizeof(uint64_t),
                                     hipMemcpyHostToDevice, ctx->stream), "hipMemcpyAsync(triangle record table)");
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize(triangle record table)");
     }
+    ctx->prim_records = want_primary;
     a.tri_records = ctx->d_tri_table;
+    set_pipe1_records(ctx, n, a);
     if (from_host && !handoff) {
         pc.valid = true;
         pc.gen = ctx->generation;
