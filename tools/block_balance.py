@@ -8,7 +8,10 @@ system HIP runtime that bench.py binds (torch is not imported).
 wcpt_set_row_stripes, rank r taking the stripes r, r + N, ...).
 
 Per N prints each block's median ms/frame, the max (what the N-GPU step waits for), the mean, and
-full-frame / N (perfect split). max / (full / N) is the load-balance + tail loss of the split.
+full-frame / N (perfect split). max / (full / N) is the load-balance + tail loss of the split. Each block's frames are
+timed as one region (WCPT_OPTION_PROFILE_REGION, as bench.py times its steps), so the frame overlap applies where its
+auto rule does (full frames, 2- and 4-way blocks; --per-render-events restores the round-5 timing, one event pair per
+render, under which the overlap is off).
 """
 import argparse
 import os
@@ -39,6 +42,7 @@ def main():
     ap.add_argument("--wf-refill", type=int, default=0, help="WCPT_OPTION_WF_REFILL (0: the library default)")
     ap.add_argument("--skip-full", action="store_true", help="do not time the full frame (full/N columns then 0)")
     ap.add_argument("--stripes", default="0", help="stripe sizes: 0 = contiguous row blocks, S = interleaved stripes")
+    ap.add_argument("--per-render-events", action="store_true", help="one event pair per render (no frame overlap)")
     a = ap.parse_args()
     name, W, H, spp, bounces, desc = bench.CONFIGS[a.config]
     s = wscene.generate(name)
@@ -50,6 +54,7 @@ def main():
     ctx.set_option(wcpt._lib.OPTION_WF_PERSIST, a.wf_persist)
     if a.wf_refill:
         ctx.set_option(wcpt._lib.OPTION_WF_REFILL, a.wf_refill)
+    ctx.set_option(wcpt._lib.OPTION_PROFILE_REGION, 0 if a.per_render_events else 1)
     dev = wcpt.DeviceScene(ctx, s)
     ctx.create_screen(W, H)
     sds = [s.scene_data(W, H, max_bounce=bounces, samples=spp, frame=f) for f in range(a.frames)]
