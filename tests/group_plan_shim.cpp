@@ -58,3 +58,27 @@ extern "C" int wait_sim(int ready_after, int error_after, int fail_at, double ti
     *naps = k;
     return (int)r;
 }
+
+// The same wait against a stream that drains at a given time (drain_ms after the call): how late the wait returns.
+extern "C" int wait_sim_time(double drain_ms, double timeout_ms, double ms_per_poll, double* elapsed_ms, int* polls,
+                             int* naps)
+{
+    double clock = 1000.0;
+    int n = 0, k = 0;
+    const double t0 = clock;
+    const wcpt::gwait::Result r = wcpt::gwait::wait_for(
+        [&]() {
+            n++;
+            clock += ms_per_poll;
+            return clock - t0 >= drain_ms ? (int)wcpt::gwait::kReady : (int)wcpt::gwait::kBusy;
+        },
+        [&]() { return false; }, t0, timeout_ms, [&]() { return clock; },
+        [&](double us) {
+            k++;
+            clock += us / 1000.0;
+        });
+    *elapsed_ms = clock - t0;
+    *polls = n;
+    *naps = k;
+    return (int)r;
+}

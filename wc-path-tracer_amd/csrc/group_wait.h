@@ -23,10 +23,13 @@ enum Poll : int { kReady = 0, kBusy = 1, kPollError = -1 };
 enum Result : int { kDone = 0, kFailed = 1, kTransportError = 2, kTimedOut = 3 };
 
 /* Spin this long after the call before the first sleep (a drained or nearly drained stream returns at once), then
- * sleep kNapMinUs, doubling up to kNapMaxUs between polls. */
+ * sleep between polls for kNapFraction of the time waited so far, within [kNapMinUs, kNapMaxUs]: a wait returns at
+ * most that fraction late. (Round 6 first doubled the nap up to 1 ms: a 7-ms wait for 20 frames then overslept by up
+ * to a millisecond, +10 % on a 20-frame bench window, profiles/r06_short_window_s20.log.) */
 constexpr double kSpinMs = 0.05;
-constexpr double kNapMinUs = 20.0;
+constexpr double kNapMinUs = 10.0;
 constexpr double kNapMaxUs = 1000.0;
+constexpr double kNapFraction = 0.005;
 
 /* Wait until poll() returns kReady. Between polls: transport_error() (true once the transport has reported an
  * asynchronous error) and the deadline `t0_ms + timeout_ms` of now_ms()'s clock (timeout_ms <= 0: no deadline, so only
@@ -35,7 +38,7 @@ constexpr double kNapMaxUs = 1000.0;
 template <class PollF, class ErrF, class NowF, class SleepF>
 Result wait_for(PollF poll, ErrF transport_error, double t0_ms, double timeout_ms, NowF now_ms, SleepF sleep_us)
 {
-    double nap = 0.0;
+    double nap;
     for (;;) {
         const int p = poll();
         if (p == kReady) return kDone;
@@ -44,8 +47,8 @@ Result wait_for(PollF poll, ErrF transport_error, double t0_ms, double timeout_m
         const double t = now_ms();
         if (timeout_ms > 0.0 && t - t0_ms >= timeout_ms) return kTimedOut;
         if (t - t0_ms < kSpinMs) continue;
-        nap = nap <= 0.0 ? kNapMinUs : (nap * 2.0 < kNapMaxUs ? nap * 2.0 : kNapMaxUs);
-        sleep_us(nap);
+        nap = (t - t0_ms) * 1000.0 * kNapFraction;
+        sleep_us(nap < kNapMinUs ? kNapMinUs : (nap > kNapMaxUs ? kNapMaxUs : nap));
     }
 }
 
