@@ -1194,13 +1194,18 @@ hipError_t launch_wavefront(const LaunchArgs& a, int mode, WfPipes& w, int pipes
     /* at most 1.4 paths per resident lane: the lanes freed by the first paths take the rest (7- / 6-way c3 splits at
      * 1.13 / 1.32 paths per lane gain 7 % / 3 %, 5-way at 1.58 is flat, 4-way at 2.0 loses) */
     const bool persist = persist_ok && (a.wf_persist > 0 || (uint64_t)a.W * a.rows * 5ull <= 64ull * 7ull * persist_full);
-    /* pipelines: the option's count, or (0, the default) one for the path-persistent trace (its blocks measured 1.30 /
-     * 1.40 / 1.40 ms with 1 / 2 / 3), else 3 when the frame holds at most 8 paths per resident trace lane -- the
-     * launches are short and their tails weigh, so a third chain overlaps them (c3 4.41-4.46 against 4.50-4.55 ms with
-     * two) -- and 2 on longer queues (c4 199.5 against 197.9 ms with two; profiles/r05_pipes_ab.log) */
+    /* pipelines: the option's count, or (0, the default) for the path-persistent trace one when each frame joins its
+     * pipelines (its blocks measured 1.30 / 1.40 / 1.40 ms with 1 / 2 / 3) and two under the frame overlap, where a
+     * pipeline's persistent launch runs on into its next frame (c3 8-way shares, slowest of 8, region-timed: 8-row
+     * stripes 1.254 / 1.246 ms with one, 1.219 / 1.218 with two, 1.218 / 1.214 with three -- a third stream would sit
+     * past the four hardware queues beside a group's communication stream; profiles/r06_c3_persist_pipes.log); else 3
+     * when the frame holds at most 8 paths per resident trace lane -- the launches are short and their tails weigh, so
+     * a third chain overlaps them (c3 4.41-4.46 against 4.50-4.55 ms with two) -- and 2 on longer queues (c4 199.5
+     * against 197.9 ms with two; profiles/r05_pipes_ab.log) */
     uint32_t K = (uint32_t)(pipes > kWfMaxPipes ? kWfMaxPipes : pipes);
     if (pipes < 1) {
-        K = persist ? 1u : ((uint64_t)a.W * a.rows <= (uint64_t)WCPT_WF_FETCH_ONCE_RATIO * 64ull * trace_grid ? 3u : 2u);
+        K = persist ? (overlap != 0 && mode == kModeRender ? 2u : 1u)
+                    : ((uint64_t)a.W * a.rows <= (uint64_t)WCPT_WF_FETCH_ONCE_RATIO * 64ull * trace_grid ? 3u : 2u);
     }
     if (sort_rays || mode == kModeDiag) K = 1; /* one sort scratch and one diagnostics block */
     const uint32_t tiles = tilesX * tilesY;
