@@ -108,9 +108,10 @@ extern "C" {
  * that follow (the launch's last round then holds the short tiles). Until the first sort: scattered when the launch
  * fits in about one round of resident waves, stripes of one tile row otherwise. Same results in every order. */
 #define WCPT_OPTION_MK_TILE_ORDER 9
-/* Wavefront: concurrent pipelines (1..4, or 0 = the default: 1 on the path-persistent trace, else 3 when the frame holds
- * at most 8 paths per resident trace lane, else 2). Pipeline j renders the 8x8 tiles t with t % K == j on its own stream, so one pipeline's trace tail (a
- * few slow rays) overlaps another's bulk. Same results. */
+/* Wavefront: concurrent pipelines (1..4, or 0 = the default: on the path-persistent trace 1, or 2 under the frame
+ * overlap; else 3 when the frame holds at most 8 paths per resident trace lane, else 2). Pipeline j renders the 8x8
+ * tiles t with t % K == j on its own stream, so one pipeline's trace tail (a few slow rays) overlaps another's bulk.
+ * Same results. */
 #define WCPT_OPTION_WF_PIPES 10
 /* Kernel timing (wcpt_profile_begin / wcpt_profile_end): 0 (default) one pair of HIP events around every render;
  * 1 two events for the whole profiled region, one before its first render and one recorded by wcpt_profile_end, so
