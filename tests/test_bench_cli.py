@@ -255,3 +255,15 @@ def test_rccl_rehearsal_flag_and_environment():
     env = {}
     bench.rccl_rehearsal_env(env, 0)
     assert env["NCCL_SOCKET_IFNAME"] == "lo" and env["NCCL_HOSTID"] == "wcpt-rehearsal-0"
+
+
+def test_frame_overlap_flag():
+    """--frame-overlap sets WCPT_OPTION_FRAME_OVERLAP on every context (-1, the default, leaves the library's auto);
+    the option id matches the header's."""
+    assert bench.parse_args([]).frame_overlap == -1
+    assert bench.parse_args(["--frame-overlap", "0"]).frame_overlap == 0
+    with pytest.raises(SystemExit):
+        bench.parse_args(["--frame-overlap", "3"])
+    import wcpt
+    hdr = open(os.path.join(ROOT, "include", "wcpt.h")).read()
+    assert "#define WCPT_OPTION_FRAME_OVERLAP 15" in hdr and wcpt._lib.OPTION_FRAME_OVERLAP == 15
