@@ -269,3 +269,36 @@ def test_overlap_option_range():
         for v in (-1, 3):
             with pytest.raises(T.WcptError):
                 ctx.set_option(T.OPTION_FRAME_OVERLAP, v)
+
+
+def _checkpoints(ov, name, kernel, frames, every):
+    s = get_scene(name)
+    W, H = 1920, 1080
+    out = []
+    with wcpt.Context(0) as ctx:
+        ctx.set_kernel(kernel)
+        ctx.set_option(T.OPTION_FRAME_OVERLAP, ov)
+        dev = wcpt.DeviceScene(ctx, s)
+        try:
+            ctx.create_screen(W, H)
+            for f in range(frames):
+                ctx.render(s.scene_data(W, H, max_bounce=4, frame=f), *dev.addresses())
+                if (f + 1) % every == 0:
+                    out.append(ctx.readback(H))        # joins the pipes mid-run; the next render forks again
+        finally:
+            dev.free()
+    return out
+
+
+@pytest.mark.parametrize("name,kernel,frames,every", [("cornell", wcpt.KERNEL_MEGAKERNEL, 200, 50),
+                                                      ("reference_init", wcpt.KERNEL_MEGAKERNEL, 140, 35),
+                                                      ("atrium", wcpt.KERNEL_WAVEFRONT, 48, 16)])
+def test_overlap_long_run_checkpoints(name, kernel, frames, every):
+    """Full 1080p frames over a long progressive run -- the re-sorts at renders 64 and 128 included -- with the image
+    read back at checkpoints (each one joins the pipes): bit-identical to the same run with the overlap off."""
+    a = _checkpoints(1, name, kernel, frames, every)
+    b = _checkpoints(0, name, kernel, frames, every)
+    assert len(a) == len(b) == frames // every
+    for x, y in zip(a, b):
+        assert np.array_equal(_bits(x), _bits(y))
+
